@@ -1,0 +1,782 @@
+"""numpy/scipy restatement of the reference hot path — TEST INFRASTRUCTURE.
+
+Reference: thomasgilgenast/hic3defdr 0.2.1 (/root/reference). Third-party
+algorithms the reference calls are restated from their published versions
+(the ones the goldens were generated with):
+
+- scipy 1.7.1 ``optimize.newton`` array secant (``zeros.py:366-462``) and
+  ``_minimize_scalar_bounded`` (``optimize.py:1982-2125``), bounded Brent;
+- scipy's C ``brentq`` (called here from the installed scipy: same algorithm);
+- lib5c 0.6.0 ``gmean`` / ``adjust_pvalues`` (statsmodels ``fdrcorrection``);
+- statsmodels lowess (``oracle/lowess_sm.py``);
+- pandas rolling variance (called directly).
+
+Special functions come from the installed scipy.special (cephes/boost,
+accurate to a few ulp); the goldens pin them to scipy 1.7.1.
+
+The oracle is never imported by the product package.
+"""
+import json
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sparse
+import scipy.special as sc
+from scipy.interpolate import interp1d
+from scipy.optimize import brentq
+
+from oracle.lowess_sm import lowess as sm_lowess
+
+# --------------------------------------------------------------------------
+# lib5c restatements
+# --------------------------------------------------------------------------
+
+
+def gmean(x, pseudocount=1, axis=None):
+    """lib5c ``gmean``; default pseudocount 1 pinned by the reference's
+    ``docs/median_of_ratios.rst:27-32``."""
+    return np.exp(np.nanmean(np.log(x + pseudocount), axis=axis)) - pseudocount
+
+
+def _fdr_bh(p):
+    """statsmodels ``fdrcorrection(method='indep')`` as called by
+    ``multipletests(method='fdr_bh')``."""
+    p = np.asarray(p)
+    order = np.argsort(p)
+    ps = p[order]
+    n = len(ps)
+    ecdf = np.arange(1, n + 1) / float(n)
+    q = np.minimum.accumulate((ps / ecdf)[::-1])[::-1]
+    q[q > 1] = 1
+    out = np.empty_like(q)
+    out[order] = q
+    return out
+
+
+def adjust_pvalues(pvalues):
+    """lib5c ``adjust_pvalues(p, method='fdr_bh')``: BH over finite p-values,
+    NaN elsewhere (used at reference ``analysis.py:300``)."""
+    q = np.ones_like(pvalues, dtype=float) * np.nan
+    idx = np.isfinite(pvalues)
+    if idx.any():
+        q[idx] = _fdr_bh(pvalues[idx])
+    return q
+
+
+# --------------------------------------------------------------------------
+# binning / scaling — reference util/binning.py, util/scaling.py
+# --------------------------------------------------------------------------
+
+
+def equal_bin(data, n_bins):
+    """``binning.py:4-25`` with the tie order pinned to stable (finding 4)."""
+    idx = np.linspace(0, n_bins, data.size, endpoint=0, dtype=int)
+    return idx[data.argsort(kind='stable').argsort(kind='stable')]
+
+
+def median_of_ratios(data, filter_zeros=True):
+    """``scaling.py:27-47``."""
+    idx = np.all(data > 0, axis=1) if filter_zeros \
+        else np.ones(data.shape[0], dtype=bool)
+    return np.median(data[idx, :] / gmean(data[idx, :], axis=1)[:, None],
+                     axis=0)
+
+
+def simple_scaling(data):
+    """``scaling.py:50-65``."""
+    s = np.sum(data, axis=0)
+    return s / gmean(s)
+
+
+def no_scaling(data):
+    """``scaling.py:10-24``."""
+    return np.ones(data.shape[1], dtype=float)
+
+
+def conditional(data, dist, fn, n_bins=None):
+    """``scaling.py:68-105``."""
+    result = np.zeros_like(data, dtype=float)
+    if n_bins:
+        bins = equal_bin(dist, n_bins)
+        d_per_bin, s_per_bin = [], []
+        for b in np.unique(bins):
+            dist_idx = bins == b
+            d_per_bin.append(np.mean(dist[dist_idx]))
+            s_per_bin.append(fn(data[dist_idx, :]))
+        for i in range(data.shape[1]):
+            result[:, i] = interp1d(np.array(d_per_bin),
+                                    np.array(s_per_bin)[:, i],
+                                    fill_value='extrapolate',
+                                    assume_sorted=True)(dist)
+    else:
+        for d in np.unique(dist):
+            dist_idx = dist == d
+            result[dist_idx, :] = fn(data[dist_idx, :])
+    return result
+
+
+def conditional_mor(data, dist, n_bins=None):
+    """``scaling.py:108-127``."""
+    return conditional(data, dist, median_of_ratios, n_bins=n_bins)
+
+
+def conditional_scaling(data, dist, n_bins=None):
+    """``scaling.py:130-149``."""
+    return conditional(data, dist, simple_scaling, n_bins=n_bins)
+
+
+NORMS = {'conditional_mor': conditional_mor,
+         'conditional_scaling': conditional_scaling,
+         'median_of_ratios': median_of_ratios,
+         'simple_scaling': simple_scaling,
+         'no_scaling': no_scaling}
+
+# --------------------------------------------------------------------------
+# sparse union — reference util/matrices.py
+# --------------------------------------------------------------------------
+
+
+def deconvolute(matrix, bias, invert=False):
+    """``matrices.py:8-38`` (including the in-place edit of ``bias``)."""
+    csr = matrix.tocsr()
+    if invert:
+        inf_idx = bias == 0
+        bias[inf_idx] = 1
+        bias = 1 / bias
+        bias[inf_idx] = 0
+    bias_csr = sparse.diags([bias], [0])
+    return bias_csr.dot(csr).dot(bias_csr)
+
+
+def wipe_distances(matrix, min_dist, max_dist):
+    """``matrices.py:41-62``."""
+    coo = matrix.tocoo()
+    dist = coo.col - coo.row
+    coo.data[(dist < min_dist) | (dist > max_dist)] = 0
+    coo.eliminate_zeros()
+    return coo
+
+
+def sparse_union(mats, dist_thresh=1000, bias=None):
+    """``matrices.py:92-129`` on already-loaded matrices (mean_thresh=0)."""
+    total = None
+    for i, m in enumerate(mats):
+        x = deconvolute(m, bias[:, i], invert=True) if bias is not None else m
+        x = wipe_distances(x / 1.0, 0, dist_thresh)
+        total = x if total is None else total + x
+    coo = total.tocoo()
+    keep = (coo.data >= 0.0) & np.isfinite(coo.data)
+    return coo.row[keep], coo.col[keep]
+
+
+# --------------------------------------------------------------------------
+# scaled NB — reference util/scaled_nb.py
+# --------------------------------------------------------------------------
+
+
+def logpmf(k, m, phi):
+    """``scaled_nb.py:12-33``."""
+    r = 1. / phi
+    return sc.gammaln(r + k) - sc.gammaln(k + 1) - sc.gammaln(r) + \
+        r * np.log(r) - r * np.log(r + m) + k * np.log(m) - \
+        k * np.log(r + m)
+
+
+def _array_secant(func, x0, tol=1.48e-8, maxiter=100):
+    """scipy 1.7.1 ``zeros._array_newton`` secant branch (zeros.py:405-434)."""
+    p = np.array(x0, copy=True, dtype=float)
+    failures = np.ones_like(p, dtype=bool)
+    nz_der = np.ones_like(failures)
+    dx = np.finfo(float).eps ** 0.33
+    p1 = p * (1 + dx) + np.where(p >= 0, dx, -dx)
+    q0 = np.asarray(func(p))
+    q1 = np.asarray(func(p1))
+    active = np.ones_like(p, dtype=bool)
+    for _ in range(maxiter):
+        nz_der = (q1 != q0)
+        if not nz_der.any():
+            p = (p1 + p) / 2.0
+            break
+        dp = (q1 * (p1 - p))[nz_der] / (q1 - q0)[nz_der]
+        p = np.asarray(p, dtype=float)
+        p[nz_der] = p1[nz_der] - dp
+        active_zero_der = ~nz_der & active
+        p[active_zero_der] = (p1 + p)[active_zero_der] / 2.0
+        active &= nz_der
+        failures[nz_der] = np.abs(dp) >= tol
+        if not failures[nz_der].any():
+            break
+        p1, p = p, p1
+        q0 = q1
+        q1 = np.asarray(func(p1))
+    zero_der = ~nz_der & failures
+    if failures.all() and not zero_der.any():
+        raise RuntimeError('all failed to converge')
+    return p, ~failures, zero_der
+
+
+def fit_mu_hat(x, b, alpha, faithful=False):
+    """``scaled_nb.py:71-183``.
+
+    ``faithful=True`` reproduces the reference's O(failed * N) brentq
+    fallback (each brentq evaluation scores every pixel, ``:173``);
+    ``faithful=False`` scores only the failed pixel (same root).
+    """
+    x = np.asarray(x)
+    b = np.asarray(b)
+    alpha = np.asarray(alpha, dtype=float)
+    assert np.all((alpha > 0) & np.isfinite(alpha))
+    assert np.all((x >= 0) & np.isfinite(x))
+    assert np.all((b > 0) & np.isfinite(b))
+
+    def f(mu_hat):
+        if hasattr(mu_hat, 'ndim') and mu_hat.ndim < b.ndim and \
+                mu_hat.ndim > 0:
+            mu_hat = mu_hat[:, None]
+        return np.sum((x - mu_hat * b) / (mu_hat + alpha * mu_hat ** 2 * b),
+                      axis=-1)
+
+    if not x.ndim == 2:
+        root = np.array([-1.0])
+        failed = np.array([True])
+    else:
+        root, converged, zero_der = _array_secant(f, np.mean(x / b, axis=1))
+        failed = ~converged | zero_der
+        failed[root <= 0] = True
+        failed[root >= np.sqrt(np.finfo(float).max) / 1e10] = True
+        failed[~np.isclose(f(root), 0, atol=1e-5)] = True
+    if np.any(failed):
+        for idx in np.where(failed)[0]:
+            lower = 10 * np.finfo(float).eps
+            upper = np.mean(x[idx] / b[idx])
+            if x.ndim != 2:
+                g = f
+            elif faithful:
+                def g(y, idx=idx):
+                    return f(y)[idx]
+            else:
+                xi, bi = x[idx], b[idx]
+                ai = np.broadcast_to(alpha, x.shape)[idx]
+
+                def g(y, xi=xi, bi=bi, ai=ai):
+                    return np.sum((xi - y * bi) / (y + ai * y ** 2 * bi))
+            counter = 0
+            while True:
+                try:
+                    root[idx] = brentq(g, lower, upper)
+                    break
+                except ValueError:
+                    upper *= 2
+                    counter += 1
+                    if counter > 100:
+                        raise ValueError('bracketing interval not found '
+                                         'within 100 doublings')
+    assert np.allclose(f(root), 0, atol=1e-5)
+    return root
+
+
+def _norm_sf(x, loc, scale):
+    return sc.ndtr(-((x - loc) / scale))
+
+
+def _norm_cdf(x, loc, scale):
+    return sc.ndtr((x - loc) / scale)
+
+
+def _norm_isf(q, loc, scale):
+    """scipy ``rv_continuous.isf`` for norm: q==0 -> +inf, q==1 -> -inf."""
+    with np.errstate(all='ignore'):
+        out = -sc.ndtri(q) * scale + loc
+    out = np.where(q == 0, np.inf, np.where(q == 1, -np.inf, out))
+    return out
+
+
+def _norm_ppf(q, loc, scale):
+    with np.errstate(all='ignore'):
+        out = sc.ndtri(q) * scale + loc
+    return np.where(q == 0, -np.inf, np.where(q == 1, np.inf, out))
+
+
+def _gamma_sf(x, a, scale):
+    """scipy gamma.sf: x<=0 -> 1 (support lower bound)."""
+    xs = x / scale
+    with np.errstate(all='ignore'):
+        out = sc.gammaincc(a, xs)
+    return np.where(xs <= 0, 1.0, out)
+
+
+def _gamma_cdf(x, a, scale):
+    xs = x / scale
+    with np.errstate(all='ignore'):
+        out = sc.gammainc(a, xs)
+    return np.where(xs <= 0, 0.0, out)
+
+
+def _gamma_isf(q, a, scale):
+    with np.errstate(all='ignore'):
+        out = sc.gammainccinv(a, q) * scale
+    return np.where(q == 0, np.inf, np.where(q == 1, 0.0, out))
+
+
+def _gamma_ppf(q, a, scale):
+    with np.errstate(all='ignore'):
+        out = sc.gammaincinv(a, q) * scale
+    return np.where(q == 0, 0.0, np.where(q == 1, np.inf, out))
+
+
+def q2qnbinom(x, mu_in, mu_out, alpha):
+    """``scaled_nb.py:217-275``. NOTE: clamps ``mu_in``/``mu_out`` IN PLACE,
+    as the reference does (the clamp of ``mu_out`` carries into the next
+    replicate inside ``equalize``)."""
+    x = np.asarray(x, dtype=float)
+    high_idx = (mu_in >= 0.25) & (mu_out >= 0.25)
+    mu_in[~high_idx] = 0.25
+    mu_out[~high_idx] = 0.25
+    r_in = 1 + alpha * mu_in
+    r_out = 1 + alpha * mu_out
+    v_in = mu_in * r_in
+    v_out = mu_out * r_out
+    right_idx = x >= mu_in
+    sd_in, sd_out = np.sqrt(v_in), np.sqrt(v_out)
+    q_norm = np.zeros_like(mu_in)
+    q_gamma = np.zeros_like(mu_in)
+    q_norm[right_idx] = _norm_isf(_norm_sf(x, mu_in, sd_in), mu_out,
+                                  sd_out)[right_idx]
+    q_norm[~right_idx] = _norm_ppf(_norm_cdf(x, mu_in, sd_in), mu_out,
+                                   sd_out)[~right_idx]
+    q_gamma[right_idx] = _gamma_isf(_gamma_sf(x, mu_in / r_in, r_in),
+                                    mu_out / r_out, r_out)[right_idx]
+    q_gamma[~right_idx] = _gamma_ppf(_gamma_cdf(x, mu_in / r_in, r_in),
+                                     mu_out / r_out, r_out)[~right_idx]
+    pseudocounts = (q_norm + q_gamma) / 2
+    pseudocounts[~(pseudocounts >= 0)] = 0
+    return pseudocounts
+
+
+def equalize(data, f, alpha, faithful=False):
+    """``scaled_nb.py:186-214``."""
+    f_mean = gmean(f, pseudocount=0, axis=1)
+    mu_hat = fit_mu_hat(data, f, alpha, faithful=faithful)
+    mu_in = mu_hat[:, None] * f
+    mu_out = mu_hat * f_mean
+    pseudodata = np.zeros_like(data, dtype=float)
+    for i in range(data.shape[1]):
+        pseudodata[:, i] = q2qnbinom(data[:, i], mu_in[:, i], mu_out, alpha)
+    return pseudodata
+
+
+# --------------------------------------------------------------------------
+# dispersion — reference util/dispersion.py
+# --------------------------------------------------------------------------
+
+_SQRT_EPS = np.sqrt(2.2e-16)
+_GOLDEN = 0.5 * (3.0 - np.sqrt(5.0))
+
+
+def minimize_scalar_bounded(func, x1, x2, xatol=1e-5, maxiter=500):
+    """scipy 1.7.1 ``_minimize_scalar_bounded`` (optimize.py:1982-2125),
+    operation for operation. Returns (x, fun, status, nfev)."""
+    maxfun = maxiter
+    flag = 0
+    a, b = x1, x2
+    fulc = a + _GOLDEN * (b - a)
+    nfc, xf = fulc, fulc
+    rat = e = 0.0
+    x = xf
+    fx = func(x)
+    num = 1
+    fu = np.inf
+    ffulc = fnfc = fx
+    xm = 0.5 * (a + b)
+    tol1 = _SQRT_EPS * np.abs(xf) + xatol / 3.0
+    tol2 = 2.0 * tol1
+    while np.abs(xf - xm) > (tol2 - 0.5 * (b - a)):
+        golden = 1
+        if np.abs(e) > tol1:
+            golden = 0
+            r = (xf - nfc) * (fx - ffulc)
+            q = (xf - fulc) * (fx - fnfc)
+            p = (xf - fulc) * q - (xf - nfc) * r
+            q = 2.0 * (q - r)
+            if q > 0.0:
+                p = -p
+            q = np.abs(q)
+            r = e
+            e = rat
+            if ((np.abs(p) < np.abs(0.5 * q * r)) and (p > q * (a - xf)) and
+                    (p < q * (b - xf))):
+                rat = (p + 0.0) / q
+                x = xf + rat
+                if ((x - a) < tol2) or ((b - x) < tol2):
+                    si = np.sign(xm - xf) + ((xm - xf) == 0)
+                    rat = tol1 * si
+            else:
+                golden = 1
+        if golden:
+            if xf >= xm:
+                e = a - xf
+            else:
+                e = b - xf
+            rat = _GOLDEN * e
+        si = np.sign(rat) + (rat == 0)
+        x = xf + si * np.maximum(np.abs(rat), tol1)
+        fu = func(x)
+        num += 1
+        if fu <= fx:
+            if x >= xf:
+                a = xf
+            else:
+                b = xf
+            fulc, ffulc = nfc, fnfc
+            nfc, fnfc = xf, fx
+            xf, fx = x, fu
+        else:
+            if x < xf:
+                a = x
+            else:
+                b = x
+            if (fu <= fnfc) or (nfc == xf):
+                fulc, ffulc = nfc, fnfc
+                nfc, fnfc = x, fu
+            elif (fu <= ffulc) or (fulc == xf) or (fulc == nfc):
+                fulc, ffulc = x, fu
+        xm = 0.5 * (a + b)
+        tol1 = _SQRT_EPS * np.abs(xf) + xatol / 3.0
+        tol2 = 2.0 * tol1
+        if num >= maxfun:
+            flag = 1
+            break
+    if np.isnan(xf) or np.isnan(fx) or np.isnan(fu):
+        flag = 2
+    return xf, fx, flag, num
+
+
+def cml(data, f=None):
+    """``dispersion.py:46-80``."""
+    if f is not None:
+        data = data / f
+    n = data.shape[1]
+    z = np.sum(data, axis=1)
+
+    def nll(delta):
+        r = 1. / delta - 1
+        return -np.sum((np.sum(sc.gammaln(data + r), axis=1) +
+                        sc.gammaln(n * r) - sc.gammaln(z + n * r) -
+                        n * sc.gammaln(r)))
+
+    x, _, flag, _ = minimize_scalar_bounded(nll, 1e-4, 100. / (100 + 1))
+    assert flag == 0
+    return x / (1 - x)
+
+
+def qcml(data, f=None, max_iter=10, tol=1e-4, faithful=False):
+    """``dispersion.py:10-43``; ``it`` is never incremented in the reference
+    so the loop runs until |delta| <= tol (a guard of 1000 iterations raises
+    instead of spinning forever)."""
+    if f is None:
+        f = np.ones_like(data, dtype=float)
+    disp = 0.01
+    delta = np.inf
+    guard = 0
+    while delta > tol:
+        pseudodata = equalize(data, f, disp, faithful=faithful)
+        new_disp = cml(pseudodata)
+        delta = np.abs(disp - new_disp)
+        disp = new_disp
+        guard += 1
+        if guard > 1000:
+            raise RuntimeError('qcml did not converge')
+        if delta < tol:
+            break
+    return disp
+
+
+def mme_per_pixel(data, f=None):
+    """``dispersion.py:83-105``."""
+    if f is not None:
+        data = data / f
+    m = np.mean(data, axis=1)
+    v = np.var(data, axis=1, ddof=1)
+    return (v - m) / m ** 2
+
+
+def mme(data, f=None):
+    """``dispersion.py:108-131``."""
+    if f is not None:
+        data = data / f
+    return np.nanmean(mme_per_pixel(data))
+
+
+ESTIMATORS = {'qcml': qcml, 'cml': cml, 'mme': mme}
+
+# --------------------------------------------------------------------------
+# lowess — reference util/lowess.py
+# --------------------------------------------------------------------------
+
+
+def lowess_fit(x, y, logx=False, logy=False, left_boundary=None,
+               right_boundary=None, frac=0.3, delta=0.01):
+    """``lowess.py:10-92``."""
+    if logx:
+        x = np.log(x)
+    if logy:
+        y = np.log(y)
+    res = sm_lowess(y, x, frac=frac, delta=(np.nanmax(x) - np.nanmin(x)) *
+                    delta)
+    sorted_x = res[:, 0]
+    sorted_y_hat = res[:, 1]
+
+    def fit(x_star):
+        new_x = np.log(x_star) if logx else x_star
+        _, idx = np.unique(sorted_x, return_index=True)
+        y_hat = interp1d(sorted_x[idx], sorted_y_hat[idx],
+                         fill_value='extrapolate', assume_sorted=True)(new_x)
+        if left_boundary is not None:
+            y_hat[x_star <= left_boundary] = sorted_y_hat[0]
+        if right_boundary is not None:
+            y_hat[x_star >= right_boundary] = sorted_y_hat[-1]
+        if logy:
+            y_hat = np.exp(y_hat)
+        return y_hat
+
+    return fit
+
+
+def weighted_lowess_fit(x, y, logx=False, logy=False, left_boundary=None,
+                        right_boundary=None, frac=None, auto_frac_factor=15.,
+                        delta=0.01, w=20, power=1. / 4,
+                        interpolate_before_increase=True):
+    """``lowess.py:95-244``."""
+    n = len(y)
+    i = np.arange(n)
+    sort_idx = np.argsort(x)
+    x = x[sort_idx].copy()
+    y = y[sort_idx].copy()
+    var = pd.Series(y).rolling(window=w, center=True).var().values
+    with np.errstate(divide='ignore'):
+        prec = 1 / var
+    weight = np.ones_like(var) * np.nan
+    weight[np.isfinite(prec)] = np.power(prec[np.isfinite(prec)], power)
+    min_weight = np.nanmin(weight)
+    scaled_weight = weight * (1 / min_weight)
+    max_weight = np.nanmax(scaled_weight)
+    scaled_weight[np.isinf(scaled_weight)] = max_weight
+    left_weight = scaled_weight[np.argmax(np.isfinite(scaled_weight))]
+    left_fill_idx = np.isnan(scaled_weight) & (i < n / 2)
+    right_fill_idx = np.isnan(scaled_weight) & (i > n / 2)
+    scaled_weight[left_fill_idx] = left_weight
+    scaled_weight[right_fill_idx] = 1
+    assert np.all(np.isfinite(scaled_weight))
+    floored_weight = np.floor(scaled_weight).astype(int)
+    inc_idx = np.argmax(np.diff(y) > 0) + 1 if interpolate_before_increase \
+        else 0
+    expanded_xs, expanded_ys = [], []
+    for j in range(inc_idx, n):
+        m = floored_weight[j]
+        expanded_xs.extend([x[j]] * m)
+        expanded_ys.extend([y[j]] * m)
+    if frac is None:
+        frac_auto = auto_frac_factor / (max_weight * np.nanmean(weight))
+        frac = max(min(frac_auto, 2. / 3), 0.05)
+    lowess_fn = lowess_fit(np.array(expanded_xs), np.array(expanded_ys),
+                           logx=logx, logy=logy, left_boundary=left_boundary,
+                           right_boundary=right_boundary, frac=frac,
+                           delta=delta)
+
+    def fit(x_star):
+        x_star = np.asarray(x_star)
+        interp_y_hat = interp1d(x, y, bounds_error=False,
+                                fill_value='extrapolate')(x_star)
+        interp_y_hat[x_star < x[0]] = y[0]
+        fit_y_hat = lowess_fn(x_star)
+        interp_idx = x_star < x[inc_idx]
+        fit_y_hat[interp_idx] = interp_y_hat[interp_idx]
+        return fit_y_hat
+
+    return fit
+
+
+# --------------------------------------------------------------------------
+# LRT — reference util/lrt.py
+# --------------------------------------------------------------------------
+
+
+def lrt(raw, f, disp, design, refit_mu=True, faithful=False):
+    """``lrt.py:7-50``."""
+    if refit_mu:
+        mu_hat_null = fit_mu_hat(raw, f, disp, faithful=faithful)
+        mu_hat_alt = np.array(
+            [fit_mu_hat(raw[:, design[:, c]], f[:, design[:, c]],
+                        disp[:, design[:, c]], faithful=faithful)
+             for c in range(design.shape[1])]).T
+    else:
+        mu_hat_null = np.mean(raw / f, axis=1)
+        mu_hat_alt = np.array(
+            [np.mean(raw[:, design[:, c]] / f[:, design[:, c]], axis=1)
+             for c in range(design.shape[1])]).T
+    mu_hat_alt_wide = np.dot(mu_hat_alt, design.T)
+    null_ll = np.sum(logpmf(raw, mu_hat_null[:, None] * f, disp), axis=1)
+    alt_ll = np.sum(logpmf(raw, mu_hat_alt_wide * f, disp), axis=1)
+    llr = null_ll - alt_ll
+    x = -2 * llr
+    df = design.shape[1] - 1
+    with np.errstate(all='ignore'):
+        pvalues = np.where(x > 0, sc.chdtrc(df, x), 1.0)
+    pvalues = np.where(np.isnan(x), np.nan, pvalues)
+    return pvalues, llr, mu_hat_null, mu_hat_alt
+
+
+# --------------------------------------------------------------------------
+# pipeline driver — reference analysis/analysis.py + analysis/core.py
+# --------------------------------------------------------------------------
+
+
+def load_bias(bias_files, bias_thresh=0.1):
+    """``core.py:35-60``."""
+    bias = np.array([np.loadtxt(fn) for fn in bias_files]).T
+    bias[(np.any(bias < bias_thresh, axis=1)) |
+         (np.any(bias > 1. / bias_thresh, axis=1)), :] = 0
+    return bias
+
+
+def load_clusters(infile):
+    """``clusters.py:176-193``."""
+    with open(infile, 'r') as handle:
+        return [set([tuple(e) for e in cluster]) for cluster in
+                json.load(handle)]
+
+
+def prepare_chrom(npz_files, bias_files, design, dist_thresh_min=4,
+                  dist_thresh_max=200, bias_thresh=0.1, mean_thresh=1.0,
+                  loop_files=None, norm='conditional_mor', n_bins=-1):
+    """``analysis.py:28-133`` for one chromosome (returns a dict)."""
+    if n_bins == -1:
+        n_bins = int(dist_thresh_max / 5)
+    bias = load_bias(bias_files, bias_thresh)
+    mats = [sparse.load_npz(fn) for fn in npz_files]
+    row, col = sparse_union(mats, dist_thresh=dist_thresh_max, bias=bias)
+    raw = np.zeros((len(row), len(mats)), dtype=int)
+    for i, m in enumerate(mats):
+        raw[:, i] = m.tocsr()[row, col]
+    balanced = np.zeros((len(row), len(mats)), dtype=float)
+    for r, m in enumerate(mats):
+        balanced[:, r] = m.tocsr()[row, col] / (bias[row, r] * bias[col, r])
+    if 'conditional' in norm:
+        size_factors = NORMS[norm](balanced, col - row, n_bins=n_bins)
+    else:
+        size_factors = NORMS[norm](balanced)
+    scaled = balanced / size_factors
+    dist = col - row
+    mean = np.dot(scaled, design) / np.sum(design, axis=0)
+    disp_idx = np.all(mean >= mean_thresh, axis=1) & (dist >= dist_thresh_min)
+    out = dict(row=row, col=col, raw=raw, size_factors=size_factors,
+               scaled=scaled, disp_idx=disp_idx)
+    if loop_files:
+        loop_pixels = set().union(*sum((load_clusters(fn)
+                                        for fn in loop_files), []))
+        out['loop_idx'] = np.array([pixel in loop_pixels for pixel in
+                                    zip(row[disp_idx], col[disp_idx])],
+                                   dtype=bool)
+    return out
+
+
+def _f_for(prep, bias):
+    sf = prep['size_factors']
+    di = prep['disp_idx']
+    row, col = prep['row'][di], prep['col'][di]
+    if sf.ndim == 2:
+        return bias[row] * bias[col] * sf[di, :]
+    return bias[row] * bias[col] * sf
+
+
+def estimate_disp(preps, biases, design, dist_thresh_max=200,
+                  estimator='qcml', frac=None, auto_frac_factor=15.,
+                  weighted_lowess=True, faithful=False):
+    """``analysis.py:135-223`` over all chromosomes (lists in chrom order).
+    Returns (disp (N_d, C), disp_per_dist (D, C), disp_fns)."""
+    est = ESTIMATORS[estimator] if isinstance(estimator, str) else estimator
+    lowess_fn = weighted_lowess_fit if weighted_lowess else lowess_fit
+    raw = np.concatenate([p['raw'][p['disp_idx']] for p in preps])
+    row = np.concatenate([p['row'][p['disp_idx']] for p in preps])
+    col = np.concatenate([p['col'][p['disp_idx']] for p in preps])
+    f = np.concatenate([_f_for(p, b) for p, b in zip(preps, biases)])
+    dist = col - row
+    D = dist_thresh_max + 1
+    C = design.shape[1]
+    disp_per_dist = np.zeros((D, C))
+    disp = np.zeros((len(raw), C))
+    fns = []
+    order = np.argsort(dist, kind='stable')
+    bounds = np.searchsorted(dist[order], np.arange(D + 1))
+    for c in range(C):
+        cols = design[:, c]
+        for d in range(D):
+            sel = order[bounds[d]:bounds[d + 1]]
+            raw_slice = raw[sel][:, cols]
+            f_slice = f[sel][:, cols]
+            if not raw_slice.size:
+                disp_per_dist[d, c] = np.nan
+            elif est is qcml:
+                disp_per_dist[d, c] = qcml(raw_slice, f=f_slice,
+                                           faithful=faithful)
+            else:
+                disp_per_dist[d, c] = est(raw_slice, f=f_slice)
+        idx = np.isfinite(disp_per_dist[:, c])
+        x = np.arange(D)[idx]
+        y = disp_per_dist[:, c][idx]
+        kw = {'left_boundary': y[0]}
+        if frac is not None:
+            kw['frac'] = frac
+        if weighted_lowess:
+            kw['auto_frac_factor'] = auto_frac_factor
+        fn = lowess_fn(x, y, **kw)
+        disp[:, c] = fn(dist)
+        fns.append(fn)
+    return disp, disp_per_dist, fns
+
+
+def run_to_qvalues(npz_files, bias_files, chroms, design, dist_thresh_min=4,
+                   dist_thresh_max=200, bias_thresh=0.1, mean_thresh=1.0,
+                   loop_files=None, norm='conditional_mor', n_bins_norm=-1,
+                   estimator='qcml', frac=None, auto_frac_factor=15.,
+                   weighted_lowess=True, refit_mu=True, faithful=False):
+    """``analysis.py:305-364``. ``npz_files[chrom]``/``bias_files[chrom]`` are
+    per-replicate file lists; ``loop_files[chrom]`` per-condition lists.
+    Returns {chrom: {stage: array}} plus 'disp_per_dist'."""
+    design = np.asarray(design, dtype=bool)
+    preps, biases = [], []
+    for chrom in chroms:
+        preps.append(prepare_chrom(
+            npz_files[chrom], bias_files[chrom], design, dist_thresh_min,
+            dist_thresh_max, bias_thresh, mean_thresh,
+            loop_files[chrom] if loop_files else None, norm, n_bins_norm))
+        biases.append(load_bias(bias_files[chrom], bias_thresh))
+    disp, disp_per_dist, _ = estimate_disp(
+        preps, biases, design, dist_thresh_max, estimator, frac,
+        auto_frac_factor, weighted_lowess, faithful)
+    out = {'disp_per_dist': disp_per_dist}
+    off = 0
+    for chrom, p, bias in zip(chroms, preps, biases):
+        n = int(p['disp_idx'].sum())
+        p['disp'] = disp[off:off + n]
+        off += n
+        f = _f_for(p, bias)
+        raw = p['raw'][p['disp_idx']]
+        pv, llr, m0, m1 = lrt(raw, f, np.dot(p['disp'], design.T), design,
+                              refit_mu=refit_mu, faithful=faithful)
+        p.update(pvalues=pv, llr=llr, mu_hat_null=m0, mu_hat_alt=m1)
+        out[chrom] = p
+    # bh — analysis.py:286-303
+    if loop_files:
+        pv = np.concatenate([out[c]['pvalues'][out[c]['loop_idx']]
+                             for c in chroms])
+    else:
+        pv = np.concatenate([out[c]['pvalues'] for c in chroms])
+    q = adjust_pvalues(pv)
+    off = 0
+    for c in chroms:
+        n = int(out[c]['loop_idx'].sum()) if loop_files else \
+            len(out[c]['pvalues'])
+        out[c]['qvalues'] = q[off:off + n]
+        off += n
+    return out

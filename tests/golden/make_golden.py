@@ -1,0 +1,271 @@
+"""Generates the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Run in this container only (the reference never travels to the GPU box):
+
+    PYTHONPATH=tests/golden/refshim:/root/reference PYTHONDONTWRITEBYTECODE=1 \
+        MPLBACKEND=agg /opt/conda/bin/python3.9 tests/golden/make_golden.py
+
+Interpreter: numpy 1.26.4, scipy 1.7.1, pandas 2.3.3, statsmodels 0.12.2.
+lib5c/dill are replaced by tests/golden/refshim (see its README).
+
+Tie-order pin (SURVEY.md finding 4): the reference's ``equal_bin``
+(``hic3defdr/util/binning.py:24-25``) uses the default unstable argsort, whose
+tie order changes with numpy's SIMD dispatch. Goldens are generated with
+``equal_bin`` patched to ``kind='stable'`` (recorded in each fixture's
+``meta_equal_bin``); the build pins the same order.
+
+Outputs (all small .npz / input files):
+- data/<name>/...           synthetic inputs in the reference layout
+- e2e_<name>.npz            every outdir array of run_to_qvalues
+- unit_special.npz          scipy.special grids (cephes, scipy 1.7.1)
+- unit_nb.npz               fit_mu_hat / q2qnbinom / equalize / cml / qcml /
+                            mme / logpmf / lrt vectors
+- unit_lowess.npz           lowess / weighted_lowess_fit / rolling var tables
+- unit_scaling.npz          conditional_mor / equal_bin vectors
+"""
+import importlib.util
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+import pandas as pd
+import scipy.special as sc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+spec = importlib.util.spec_from_file_location(
+    'synthetic', os.path.join(REPO, 'hic3defdr_amd', 'synthetic.py'))
+synthetic = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(synthetic)
+
+import hic3defdr.util.scaling as scaling  # noqa: E402
+
+
+def equal_bin_stable(data, n_bins):
+    idx = np.linspace(0, n_bins, data.size, endpoint=0, dtype=int)
+    return idx[data.argsort(kind='stable').argsort(kind='stable')]
+
+
+scaling.equal_bin = equal_bin_stable
+
+from hic3defdr import HiC3DeFDR  # noqa: E402
+from hic3defdr.util import scaled_nb, dispersion  # noqa: E402
+from hic3defdr.util import lrt as lrt_mod  # noqa: E402
+from hic3defdr.util import lowess as lowess_mod  # noqa: E402
+from statsmodels.nonparametric.smoothers_lowess import lowess as sm_lowess  # noqa: E402,E501
+
+STAGES = ['row', 'col', 'raw', 'size_factors', 'scaled', 'disp_idx',
+          'loop_idx', 'disp', 'pvalues', 'llr', 'mu_hat_null', 'mu_hat_alt',
+          'qvalues']
+
+E2E = {
+    # name: (chrom sizes, dist_thresh_max, n_per_cond, seed, use loops)
+    'small2': ({'chrA': 420, 'chrB': 300}, 50, (2, 2), 0, True),
+    'c3r9': ({'chrC': 260}, 40, (3, 3, 3), 1, False),
+}
+
+
+def run_e2e(name):
+    sizes, dmax, npc, seed, loops = E2E[name]
+    base = os.path.join(HERE, 'data', name)
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, sizes, dist_thresh_max=dmax,
+                                 n_per_cond=npc, seed=seed,
+                                 clusters_per_chrom=12)
+    # store paths relative to the repo so tests can relocate them
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_out_' + name)
+    shutil.rmtree(outdir, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax,
+                  loop_patterns=kw['loop_patterns'] if loops else None,
+                  res=10000)
+    h.run_to_qvalues(n_threads=0, verbose=False)
+    out = {'meta_equal_bin': np.array('stable'),
+           'meta_chroms': np.array(kw['chroms']),
+           'meta_reps': np.array(kw['reps']),
+           'meta_conds': np.array(kw['conds']),
+           'meta_design': kw['design'],
+           'meta_dist_thresh_max': np.array(dmax),
+           'meta_loops': np.array(loops)}
+    for chrom in kw['chroms']:
+        for st in STAGES:
+            fn = os.path.join(outdir, '%s_%s.npy' % (st, chrom))
+            if os.path.exists(fn):
+                out['%s__%s' % (st, chrom)] = np.load(fn)
+    out['disp_per_dist'] = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
+    # the fitted disp function evaluated on every integer distance
+    for c, cond in enumerate(kw['conds']):
+        fn = h.load_disp_fn(cond)
+        out['disp_fn_table__%s' % cond] = fn(np.arange(dmax + 1))
+    np.savez_compressed(os.path.join(HERE, 'e2e_%s.npz' % name), **out)
+    print(name, 'pixels', sum(len(out['row__%s' % c]) for c in kw['chroms']),
+          'disp px', sum(len(out['pvalues__%s' % c]) for c in kw['chroms']))
+
+
+def unit_special():
+    rng = np.random.default_rng(11)
+    a = np.concatenate([10 ** rng.uniform(-3, 0, 400), rng.uniform(0.5, 30, 600),
+                        10 ** rng.uniform(1.3, 3.3, 300)])
+    x = a * np.exp(rng.normal(0, 0.6, a.size))
+    x2 = 10 ** rng.uniform(-4, 3.5, a.size)
+    x = np.concatenate([x, x2])
+    a = np.concatenate([a, a])
+    p = np.concatenate([10 ** rng.uniform(-300, -1, 500), rng.uniform(0, 1, 1500),
+                        1 - 10 ** rng.uniform(-15, -1, 600)])[:a.size]
+    p = np.clip(p, 1e-300, 1 - 1e-16)
+    z = np.concatenate([rng.normal(0, 3, 1000), rng.uniform(-38, 38, 500)])
+    g = np.concatenate([10 ** rng.uniform(-4, 5, 2000), rng.uniform(0, 30, 1000),
+                        np.arange(1, 60, dtype=float)])
+    pq = np.concatenate([10 ** rng.uniform(-300, -1, 600), rng.uniform(0, 1, 600)])
+    llr = np.concatenate([-10 ** rng.uniform(-8, 3, 800), [0.0, 1e-300, 5.0]])
+    out = dict(a=a, x=x, p=p, z=z, g=g, pq=pq, llr=llr,
+               gammainc=sc.gammainc(a, x), gammaincc=sc.gammaincc(a, x),
+               gammaincinv=sc.gammaincinv(a, p),
+               gammainccinv=sc.gammainccinv(a, p),
+               ndtr=sc.ndtr(z), ndtri=sc.ndtri(pq), gammaln=sc.gammaln(g),
+               chi2_sf_df1=__import__('scipy.stats').stats.chi2(1).sf(-2 * llr),
+               chi2_sf_df2=__import__('scipy.stats').stats.chi2(2).sf(-2 * llr))
+    np.savez_compressed(os.path.join(HERE, 'unit_special.npz'), **out)
+
+
+def unit_nb():
+    rng = np.random.default_rng(12)
+    out = {}
+    # fit_mu_hat on random (x, b, alpha) incl. cases that fall back to brentq
+    n, R = 400, 4
+    mu = 10 ** rng.uniform(-0.5, 2.5, n)
+    b = np.exp(rng.normal(0, 0.5, (n, R)))
+    alpha = 10 ** rng.uniform(-3, 0, (n, R))
+    x = rng.negative_binomial(1 / alpha, 1 / (1 + alpha * mu[:, None] * b))
+    x[x.sum(axis=1) == 0, 0] = 1
+    out.update(fmh_x=x, fmh_b=b, fmh_alpha=alpha,
+               fmh_mu=scaled_nb.fit_mu_hat(x, b, alpha, verbose=False))
+    out['fmh_mu_scalar_alpha'] = scaled_nb.fit_mu_hat(x, b, 0.05,
+                                                      verbose=False)
+    # q2qnbinom incl. means below 0.25 and large counts
+    m = 2000
+    xq = np.concatenate([rng.integers(0, 5, m // 2),
+                         rng.integers(0, 3000, m // 2)]).astype(float)
+    mu_in = np.concatenate([10 ** rng.uniform(-2, 1, m // 2),
+                            10 ** rng.uniform(0, 3.3, m // 2)])
+    mu_out = mu_in * np.exp(rng.normal(0, 0.4, m))
+    al = 10 ** rng.uniform(-3, 1, m)
+    out.update(q2q_x=xq, q2q_mu_in=mu_in.copy(), q2q_mu_out=mu_out.copy(),
+               q2q_alpha=al)
+    out['q2q'] = scaled_nb.q2qnbinom(xq, mu_in.copy(), mu_out.copy(), al)
+    # per-segment cml / qcml / mme / equalize
+    segs = []
+    for s in range(24):
+        npx = int(rng.integers(5, 400))
+        Rc = int(rng.integers(2, 5))
+        mu = 10 ** rng.uniform(0, 2.5, npx)
+        f = np.exp(rng.normal(0, 0.3, (npx, Rc)))
+        a_true = 10 ** rng.uniform(-2.5, -0.5)
+        data = rng.negative_binomial(1 / a_true,
+                                     1 / (1 + a_true * mu[:, None] * f))
+        data[data.sum(axis=1) == 0, 0] = 1
+        segs.append((data, f))
+        out['seg%d_data' % s] = data
+        out['seg%d_f' % s] = f
+        out['seg%d_equalize' % s] = scaled_nb.equalize(data, f, 0.02)
+        out['seg%d_cml' % s] = dispersion.cml(data.astype(float) / f)
+        out['seg%d_qcml' % s] = dispersion.qcml(data, f=f)
+        out['seg%d_mme' % s] = dispersion.mme(data.astype(float), f=f.copy())
+    out['n_segs'] = np.array(len(segs))
+    # logpmf + lrt
+    k = rng.integers(0, 500, (300, 4))
+    mm = 10 ** rng.uniform(-1, 3, (300, 4))
+    ph = 10 ** rng.uniform(-3, 0.5, (300, 4))
+    out.update(lp_k=k, lp_m=mm, lp_phi=ph, logpmf=scaled_nb.logpmf(k, mm, ph))
+    design = np.array([[1, 0], [1, 0], [0, 1], [0, 1]], dtype=bool)
+    mu = 10 ** rng.uniform(0, 2.5, 600)
+    f = np.exp(rng.normal(0, 0.3, (600, 4)))
+    disp = np.repeat(10 ** rng.uniform(-2, -0.5, (600, 2)), 2, axis=1)
+    raw = rng.negative_binomial(1 / disp, 1 / (1 + disp * mu[:, None] * f))
+    raw[raw[:, :2].sum(axis=1) == 0, 0] = 1
+    raw[raw[:, 2:].sum(axis=1) == 0, 2] = 1
+    p, llr, m0, m1 = lrt_mod.lrt(raw, f, disp, design)
+    out.update(lrt_raw=raw, lrt_f=f, lrt_disp=disp, lrt_design=design,
+               lrt_p=p, lrt_llr=llr, lrt_mu0=m0, lrt_mu1=m1)
+    p, llr, m0, m1 = lrt_mod.lrt(raw, f, disp, design, refit_mu=False)
+    out.update(lrtnr_p=p, lrtnr_llr=llr, lrtnr_mu0=m0, lrtnr_mu1=m1)
+    np.savez_compressed(os.path.join(HERE, 'unit_nb.npz'), **out)
+
+
+def unit_lowess():
+    rng = np.random.default_rng(13)
+    out = {}
+    for t in range(6):
+        D = int(rng.integers(40, 420))
+        x = np.arange(4, D + 1)
+        y = 0.02 + 0.3 / (x ** 1.2) + 0.004 * rng.normal(size=x.size) + \
+            0.0001 * x / D
+        y[:3] += np.array([0.05, 0.02, 0.005])
+        y = np.abs(y)
+        fn = lowess_mod.weighted_lowess_fit(x, y, left_boundary=y[0],
+                                            auto_frac_factor=15.)
+        out['wl%d_x' % t] = x
+        out['wl%d_y' % t] = y
+        out['wl%d_table' % t] = fn(np.arange(D + 1))
+        fn2 = lowess_mod.lowess_fit(x, y, left_boundary=y[0])
+        out['ul%d_table' % t] = fn2(np.arange(D + 1))
+        var = pd.Series(y).rolling(window=20, center=True).var().values
+        out['wl%d_rollvar' % t] = var
+    for t in range(6):
+        n = int(rng.integers(30, 700))
+        xs = np.sort(rng.integers(0, 200, n)).astype(float) if t % 2 \
+            else np.sort(rng.uniform(0, 50, n))
+        ys = np.sin(xs / 7.0) + rng.normal(0, 0.3, n)
+        frac = float(rng.uniform(0.05, 0.7))
+        delta = 0.01 * (xs.max() - xs.min())
+        out['lo%d_x' % t] = xs
+        out['lo%d_y' % t] = ys
+        out['lo%d_frac' % t] = np.array(frac)
+        out['lo%d_delta' % t] = np.array(delta)
+        out['lo%d_res' % t] = sm_lowess(ys, xs, frac=frac, delta=delta)
+    np.savez_compressed(os.path.join(HERE, 'unit_lowess.npz'), **out)
+
+
+def unit_scaling():
+    rng = np.random.default_rng(14)
+    out = {}
+    for t in range(4):
+        n = int(rng.integers(500, 3000))
+        dist = np.sort(rng.integers(0, 60, n))
+        rng.shuffle(dist)
+        data = np.exp(rng.normal(2, 1, (n, 4))) * (rng.random((n, 4)) > 0.1)
+        nb = int(rng.integers(3, 15))
+        out['cm%d_data' % t] = data
+        out['cm%d_dist' % t] = dist
+        out['cm%d_nbins' % t] = np.array(nb)
+        out['cm%d_sf' % t] = scaling.conditional_mor(data, dist, n_bins=nb)
+        out['cm%d_sf_exact' % t] = scaling.conditional_mor(data, dist)
+        out['cm%d_eqbin' % t] = equal_bin_stable(dist, nb)
+    np.savez_compressed(os.path.join(HERE, 'unit_scaling.npz'), **out)
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling']
+    if 'e2e' in which:
+        for name in E2E:
+            run_e2e(name)
+    if 'special' in which:
+        unit_special()
+    if 'nb' in which:
+        unit_nb()
+    if 'lowess' in which:
+        unit_lowess()
+    if 'scaling' in which:
+        unit_scaling()
+    json.dump({'numpy': np.__version__,
+               'scipy': __import__('scipy').__version__,
+               'pandas': pd.__version__,
+               'statsmodels': __import__('statsmodels').__version__,
+               'python': sys.version.split()[0],
+               'equal_bin': 'stable'},
+              open(os.path.join(HERE, 'versions.json'), 'w'), indent=1)
