@@ -1,0 +1,134 @@
+// Host build of the device numerics, for CPU unit tests ONLY.
+//
+// The same headers the gfx950 kernels include (h3d_special.h, h3d_model.h)
+// compiled with g++ and exported over a flat C ABI so tests/ can check them
+// against scipy / the oracle without a GPU. The product never loads this
+// library (hic3defdr_amd loads libh3d.so and fails loudly without it).
+#include <cstdint>
+
+#include "h3d_model.h"
+#include "h3d_special.h"
+
+extern "C" {
+
+#define H3DT_UNARY(name, fn)                                   \
+  void h3dt_##name(int64_t n, const double* x, double* out) { \
+    for (int64_t i = 0; i < n; ++i) out[i] = h3d::fn(x[i]);   \
+  }
+#define H3DT_BINARY(name, fn)                                              \
+  void h3dt_##name(int64_t n, const double* a, const double* x,           \
+                   double* out) {                                          \
+    for (int64_t i = 0; i < n; ++i) out[i] = h3d::fn(a[i], x[i]);         \
+  }
+
+H3DT_UNARY(lgam, lgam)
+H3DT_UNARY(ndtr, ndtr)
+H3DT_UNARY(ndtri, ndtri)
+H3DT_UNARY(log1pmx, log1pmx)
+H3DT_UNARY(lgam1p, lgam1p)
+H3DT_BINARY(igam, igam)
+H3DT_BINARY(igamc, igamc)
+H3DT_BINARY(igami, igami)
+H3DT_BINARY(igamci, igamci)
+H3DT_BINARY(chi2_sf, chi2_sf)
+
+// fit_mu_hat per pixel: x (n, r) int32, b (n, r), alpha (n, r) -> mu (n)
+int h3dt_fit_mu(int64_t n, int r, const int32_t* x, const double* b,
+                const double* alpha, double* mu) {
+  int bad = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double xs[h3d::kMaxReps], bs[h3d::kMaxReps], as[h3d::kMaxReps];
+    for (int k = 0; k < r; ++k) {
+      xs[k] = x[i * r + k];
+      bs[k] = b[i * r + k];
+      as[k] = alpha[i * r + k];
+    }
+    int st = 0;
+    mu[i] = h3d::fit_mu(xs, bs, as, r, &st);
+    bad |= st;
+  }
+  return bad;
+}
+
+// q2qnbinom elementwise (no in-place clamp carry; single replicate)
+void h3dt_q2q(int64_t n, const double* x, const double* mu_in,
+              const double* mu_out, const double* alpha, double* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    double mi = mu_in[i], mo = mu_out[i];
+    out[i] = h3d::q2q(x[i], &mi, &mo, alpha[i]);
+  }
+}
+
+// equalize one segment: data (n, r) int32, f (n, r), scalar alpha
+int h3dt_equalize(int64_t n, int r, const int32_t* x, const double* f,
+                  double alpha, double* out) {
+  int bad = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double xs[h3d::kMaxReps], fs[h3d::kMaxReps], ps[h3d::kMaxReps];
+    for (int k = 0; k < r; ++k) {
+      xs[k] = x[i * r + k];
+      fs[k] = f[i * r + k];
+    }
+    bad |= h3d::equalize_pixel(xs, fs, r, alpha, ps);
+    for (int k = 0; k < r; ++k) out[i * r + k] = ps[k];
+  }
+  return bad;
+}
+
+// per-pixel LRT with per-replicate dispersions (lrt.py:7-50)
+int h3dt_lrt(int64_t n, int R, int C, const int32_t* raw, const double* f,
+             const double* disp_wide, const int32_t* cond_of_rep, int refit,
+             double* p, double* llr, double* mu0, double* mu1) {
+  int bad = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double xs[h3d::kMaxReps], fs[h3d::kMaxReps], as[h3d::kMaxReps];
+    for (int k = 0; k < R; ++k) {
+      xs[k] = raw[i * R + k];
+      fs[k] = f[i * R + k];
+      as[k] = disp_wide[i * R + k];
+    }
+    double m1[h3d::kMaxConds];
+    bad |= h3d::lrt_pixel(xs, fs, as, cond_of_rep, R, C, refit != 0, &p[i],
+                          &llr[i], &mu0[i], m1);
+    for (int c = 0; c < C; ++c) mu1[i * C + c] = m1[c];
+  }
+  return bad;
+}
+
+// cml NLL per-pixel term (dispersion.py:67-70) summed over a segment
+double h3dt_nll(int64_t n, int r, const double* data, double delta) {
+  double s = 0.0;
+  h3d::NllConst k = h3d::nll_const(delta, r);
+  for (int64_t i = 0; i < n; ++i) s += h3d::nll_pixel(data + i * r, r, k);
+  return -s;
+}
+
+// full qcml on one segment with the shared Brent state machine
+double h3dt_qcml(int64_t n, int r, const int32_t* x, const double* f,
+                 int* status) {
+  double* pseudo = new double[n * r];
+  h3d::SegState st;
+  h3d::seg_init(&st, n);
+  int guard = 0;
+  while (st.phase != h3d::kDone && guard++ < 100000) {
+    double total = 0.0;
+    if (st.phase == h3d::kEqualize) {
+      for (int64_t i = 0; i < n; ++i) {
+        double xs[h3d::kMaxReps], fs[h3d::kMaxReps];
+        for (int k = 0; k < r; ++k) {
+          xs[k] = x[i * r + k];
+          fs[k] = f[i * r + k];
+        }
+        st.flags |= h3d::equalize_pixel(xs, fs, r, st.disp, pseudo + i * r);
+      }
+    }
+    h3d::NllConst kc = h3d::nll_const(st.x, r);
+    for (int64_t i = 0; i < n; ++i) total += h3d::nll_pixel(pseudo + i * r, r, kc);
+    h3d::seg_step(&st, total);
+  }
+  delete[] pseudo;
+  *status = st.flags;
+  return st.result;
+}
+
+}  // extern "C"

@@ -1,0 +1,429 @@
+// Scaled negative-binomial model pieces shared by the gfx950 kernels and the
+// host unit-test build. Each function cites the reference code it restates
+// (reference = thomasgilgenast/hic3defdr 0.2.1).
+#pragma once
+
+#include <cmath>
+
+#include "h3d_special.h"
+
+namespace h3d {
+
+constexpr int kMaxReps = 32;   // replicates per pixel (R)
+constexpr int kMaxConds = 8;   // conditions (C)
+
+// status flags (OR-ed per pixel / per segment, reported by the C ABI)
+constexpr int kFlagNoRoot = 1;     // all-zero counts: no MLE (ref: ValueError)
+constexpr int kFlagNoConv = 2;     // MLE solver did not converge
+constexpr int kFlagBrentFail = 4;  // bounded Brent not successful (ref: assert)
+constexpr int kFlagQcmlGuard = 8;  // qcml exceeded 1000 iterations
+constexpr int kFlagBadInput = 16;  // alpha/b not positive finite (ref: assert)
+
+// numpy's row-sum association for short contiguous rows (pairwise_sum with
+// n <= 128: sequential below 8, eight accumulators from 8 on).
+H3D_HD double np_sum(const double* v, int n) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += v[i];
+    return res;
+  }
+  double r0 = v[0], r1 = v[1], r2 = v[2], r3 = v[3], r4 = v[4], r5 = v[5],
+         r6 = v[6], r7 = v[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += v[i];
+    r1 += v[i + 1];
+    r2 += v[i + 2];
+    r3 += v[i + 3];
+    r4 += v[i + 4];
+    r5 += v[i + 5];
+    r6 += v[i + 6];
+    r7 += v[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += v[i];
+  return res;
+}
+
+// MLE of mu under fixed per-replicate dispersion: root of
+//   S(mu) = sum_k (x_k - mu b_k) / (mu + a_k mu^2 b_k)      (scaled_nb.py:143-147)
+// The reference finds it with scipy's array secant + a brentq fallback
+// (scaled_nb.py:149-181). The log-likelihood is strictly concave in
+// theta = log(mu), so the root is unique; here it is found per lane by
+// Newton on g(theta) = mu S(mu) inside a shrinking bracket (bisection
+// safeguard), to full double precision.
+H3D_HD double fit_mu(const double* x, const double* b, const double* a, int r,
+                     int* status) {
+  double sx = 0.0, init = 0.0;
+  for (int k = 0; k < r; ++k) {
+    if (!(a[k] > 0.0) || !(b[k] > 0.0) || is_inf(a[k]) || is_inf(b[k]) ||
+        !(x[k] >= 0.0)) {
+      *status |= kFlagBadInput;
+      return NAN;
+    }
+    sx += x[k];
+    init += x[k] / b[k];
+  }
+  if (!(sx > 0.0)) {
+    *status |= kFlagNoRoot;
+    return NAN;
+  }
+  double th = log(init / r);
+  double lo = -INFINITY, hi = INFINITY;
+  for (int it = 0; it < 200; ++it) {
+    double mu = exp(th);
+    double g = 0.0, gp = 0.0;
+    for (int k = 0; k < r; ++k) {
+      double mb = mu * b[k];
+      double den = 1.0 / (1.0 + a[k] * mb);
+      g += (x[k] - mb) * den;
+      gp -= mb * (1.0 + a[k] * x[k]) * den * den;
+    }
+    if (g > 0.0)
+      lo = th;
+    else if (g < 0.0)
+      hi = th;
+    else
+      return mu;
+    double tn = th - g / gp;
+    if (!(tn > lo && tn < hi)) {
+      if (is_inf(lo))
+        tn = hi - 2.0;
+      else if (is_inf(hi))
+        tn = lo + 2.0;
+      else
+        tn = 0.5 * (lo + hi);
+    }
+    double step = fabs(tn - th);
+    th = tn;
+    if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp(th);
+    if (!is_inf(lo) && !is_inf(hi) && (hi - lo) <= 4e-16 * fmax(1.0, fabs(th)))
+      return exp(th);
+  }
+  *status |= kFlagNoConv;
+  return exp(th);
+}
+
+// ---- scipy.stats frozen-distribution methods as the reference calls them
+// (rv_continuous.sf/cdf/isf/ppf edge handling of scipy 1.7.1) ------------
+
+H3D_HD double norm_sf(double x, double loc, double scale) {
+  return ndtr(-((x - loc) / scale));
+}
+H3D_HD double norm_cdf(double x, double loc, double scale) {
+  return ndtr((x - loc) / scale);
+}
+H3D_HD double norm_isf(double q, double loc, double scale) {
+  if (q != q) return NAN;
+  if (q == 0.0) return INFINITY;
+  if (q == 1.0) return -INFINITY;
+  return -ndtri(q) * scale + loc;
+}
+H3D_HD double norm_ppf(double q, double loc, double scale) {
+  if (q != q) return NAN;
+  if (q == 0.0) return -INFINITY;
+  if (q == 1.0) return INFINITY;
+  return ndtri(q) * scale + loc;
+}
+H3D_HD double gamma_sf(double x, double shape, double scale) {
+  double xs = x / scale;
+  if (xs <= 0.0) return 1.0;
+  return igamc(shape, xs);
+}
+H3D_HD double gamma_cdf(double x, double shape, double scale) {
+  double xs = x / scale;
+  if (xs <= 0.0) return 0.0;
+  return igam(shape, xs);
+}
+H3D_HD double gamma_isf(double q, double shape, double scale) {
+  if (q != q) return NAN;
+  if (q == 0.0) return INFINITY;
+  if (q == 1.0) return 0.0;
+  return igamci(shape, q) * scale;
+}
+H3D_HD double gamma_ppf(double q, double shape, double scale) {
+  if (q != q) return NAN;
+  if (q == 0.0) return 0.0;
+  if (q == 1.0) return INFINITY;
+  return igami(shape, q) * scale;
+}
+
+// q2qnbinom for one value (scaled_nb.py:217-275). mu_in / mu_out are
+// clamped IN PLACE exactly as the reference does (:240-242) so the caller can
+// carry the mu_out clamp into the next replicate (equalize, :209-213).
+H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
+  if (!((*mu_in >= 0.25) && (*mu_out >= 0.25))) {
+    *mu_in = 0.25;
+    *mu_out = 0.25;
+  }
+  const double mi = *mu_in, mo = *mu_out;
+  const double r_in = 1 + alpha * mi, r_out = 1 + alpha * mo;
+  const double v_in = mi * r_in, v_out = mo * r_out;
+  const double sd_in = sqrt(v_in), sd_out = sqrt(v_out);
+  const double a_in = mi / r_in, a_out = mo / r_out;
+  double qn, qg;
+  if (x >= mi) {
+    qn = norm_isf(norm_sf(x, mi, sd_in), mo, sd_out);
+    qg = gamma_isf(gamma_sf(x, a_in, r_in), a_out, r_out);
+  } else {
+    qn = norm_ppf(norm_cdf(x, mi, sd_in), mo, sd_out);
+    qg = gamma_ppf(gamma_cdf(x, a_in, r_in), a_out, r_out);
+  }
+  double pc = (qn + qg) / 2;
+  if (!(pc >= 0.0)) pc = 0.0;
+  return pc;
+}
+
+// equalize for one pixel (scaled_nb.py:186-214) with a scalar dispersion.
+H3D_HD int equalize_pixel(const double* x, const double* f, int r, double alpha,
+                          double* out) {
+  double lf[kMaxReps], as[kMaxReps];
+  for (int k = 0; k < r; ++k) {
+    lf[k] = log(f[k]);
+    as[k] = alpha;
+  }
+  // gmean(f, pseudocount=0, axis=1) = exp(nanmean(log f)) - 0
+  const double f_mean = exp(np_sum(lf, r) / r) - 0.0;
+  int st = 0;
+  const double mu = fit_mu(x, f, as, r, &st);
+  double mu_out = mu * f_mean;
+  for (int k = 0; k < r; ++k) {
+    double mu_in = mu * f[k];
+    out[k] = q2q(x[k], &mu_in, &mu_out, alpha);
+  }
+  return st;
+}
+
+// NB log pmf, mean/dispersion parameterisation (scaled_nb.py:12-33).
+H3D_HD double logpmf(double k, double m, double phi) {
+  const double r = 1.0 / phi;
+  const double lr = log(r + m);
+  return lgam(r + k) - lgam(k + 1) - lgam(r) + r * log(r) - r * lr +
+         k * log(m) - k * lr;
+}
+
+// Per-pixel LRT (lrt.py:7-50). a[k] = disp_wide[k] = disp[cond(k)].
+H3D_HD int lrt_pixel(const double* x, const double* f, const double* a,
+                     const int* cond_of_rep, int R, int C, bool refit,
+                     double* p, double* llr, double* mu0, double* mu1) {
+  int st = 0;
+  if (refit) {
+    *mu0 = fit_mu(x, f, a, R, &st);
+    for (int c = 0; c < C; ++c) {
+      double xs[kMaxReps], fs[kMaxReps], as[kMaxReps];
+      int n = 0;
+      for (int k = 0; k < R; ++k)
+        if (cond_of_rep[k] == c) {
+          xs[n] = x[k];
+          fs[n] = f[k];
+          as[n] = a[k];
+          ++n;
+        }
+      mu1[c] = fit_mu(xs, fs, as, n, &st);
+    }
+  } else {
+    double q[kMaxReps];
+    for (int k = 0; k < R; ++k) q[k] = x[k] / f[k];
+    *mu0 = np_sum(q, R) / R;
+    for (int c = 0; c < C; ++c) {
+      double qs[kMaxReps];
+      int n = 0;
+      for (int k = 0; k < R; ++k)
+        if (cond_of_rep[k] == c) qs[n++] = q[k];
+      mu1[c] = np_sum(qs, n) / n;
+    }
+  }
+  double tn[kMaxReps], ta[kMaxReps];
+  for (int k = 0; k < R; ++k) {
+    tn[k] = logpmf(x[k], *mu0 * f[k], a[k]);
+    ta[k] = logpmf(x[k], mu1[cond_of_rep[k]] * f[k], a[k]);
+  }
+  *llr = np_sum(tn, R) - np_sum(ta, R);
+  *p = chi2_sf((double)(C - 1), -2 * *llr);
+  return st;
+}
+
+// ---- cml negative log likelihood (dispersion.py:67-70) -------------------
+
+struct NllConst {
+  double r, nr, lg_nr, n_lg_r;
+};
+
+H3D_HD NllConst nll_const(double delta, int n) {
+  NllConst k;
+  k.r = 1. / delta - 1;
+  k.nr = n * k.r;
+  k.lg_nr = lgam(k.nr);
+  k.n_lg_r = n * lgam(k.r);
+  return k;
+}
+
+// one pixel's term; nll(delta) = -sum over pixels.
+H3D_HD double nll_pixel(const double* d, int n, const NllConst& k) {
+  double lg[kMaxReps];
+  for (int j = 0; j < n; ++j) lg[j] = lgam(d[j] + k.r);
+  const double z = np_sum(d, n);
+  return np_sum(lg, n) + k.lg_nr - lgam(z + k.nr) - k.n_lg_r;
+}
+
+// ---- qcml + bounded Brent as a resumable state machine --------------------
+// qcml (dispersion.py:10-43): disp = 0.01; repeat { equalize; cml } until
+// |disp - new| <= 1e-4 (``it`` is never incremented in the reference; a
+// 1000-iteration guard raises instead of spinning).
+// cml (dispersion.py:46-80): minimize_scalar(nll, bounds=(1e-4, 100/101),
+// method='bounded') = scipy 1.7.1 _minimize_scalar_bounded
+// (optimize.py:1982-2125, xatol=1e-5, maxiter=500), restated op for op.
+// Every NLL evaluation is one data pass; seg_step consumes its result.
+
+constexpr int kEqualize = 0;  // next pass: equalize at disp, then NLL at x0
+constexpr int kNll = 1;       // next pass: NLL at x
+constexpr int kDone = 2;
+
+constexpr double kBrentA = 1e-4;
+constexpr double kBrentB = 100. / (100 + 1);
+constexpr double kXatol = 1e-5;
+constexpr int kMaxFun = 500;
+
+struct SegState {
+  int phase;
+  int flags;
+  int num;
+  int qiter;
+  double disp;    // current qcml dispersion (used by the equalize pass)
+  double x;       // delta at which the next NLL is evaluated
+  double result;  // final qcml dispersion (NaN for an empty segment)
+  double a, b, xf, fx, nfc, fnfc, fulc, ffulc, e, rat, xm, tol1, tol2, fu;
+};
+
+H3D_HD double brent_sqrt_eps() { return sqrt(2.2e-16); }
+H3D_HD double brent_golden() { return 0.5 * (3.0 - sqrt(5.0)); }
+H3D_HD double brent_x0() {
+  return kBrentA + brent_golden() * (kBrentB - kBrentA);
+}
+
+H3D_HD void seg_init(SegState* s, long long n_px) {
+  s->flags = 0;
+  s->num = 0;
+  s->qiter = 0;
+  s->disp = 0.01;
+  s->x = brent_x0();
+  s->result = NAN;
+  s->phase = (n_px > 0) ? kEqualize : kDone;
+}
+
+H3D_HD double sgn(double v) { return (v > 0) - (v < 0); }
+
+// Advance with the NLL pixel-term total evaluated at s->x.
+H3D_HD void seg_step(SegState* s, double total) {
+  const double sqrt_eps = brent_sqrt_eps();
+  const double golden_mean = brent_golden();
+  const double fval = -total;
+  bool finished = false;
+  if (s->phase == kEqualize) {
+    s->a = kBrentA;
+    s->b = kBrentB;
+    s->fulc = s->a + golden_mean * (s->b - s->a);
+    s->nfc = s->xf = s->fulc;
+    s->rat = s->e = 0.0;
+    s->fx = fval;
+    s->num = 1;
+    s->fu = INFINITY;
+    s->ffulc = s->fnfc = s->fx;
+    s->xm = 0.5 * (s->a + s->b);
+    s->tol1 = sqrt_eps * fabs(s->xf) + kXatol / 3.0;
+    s->tol2 = 2.0 * s->tol1;
+  } else {
+    const double x = s->x, fu = fval;
+    s->fu = fu;
+    s->num += 1;
+    if (fu <= s->fx) {
+      if (x >= s->xf)
+        s->a = s->xf;
+      else
+        s->b = s->xf;
+      s->fulc = s->nfc;
+      s->ffulc = s->fnfc;
+      s->nfc = s->xf;
+      s->fnfc = s->fx;
+      s->xf = x;
+      s->fx = fu;
+    } else {
+      if (x < s->xf)
+        s->a = x;
+      else
+        s->b = x;
+      if ((fu <= s->fnfc) || (s->nfc == s->xf)) {
+        s->fulc = s->nfc;
+        s->ffulc = s->fnfc;
+        s->nfc = x;
+        s->fnfc = fu;
+      } else if ((fu <= s->ffulc) || (s->fulc == s->xf) || (s->fulc == s->nfc)) {
+        s->fulc = x;
+        s->ffulc = fu;
+      }
+    }
+    s->xm = 0.5 * (s->a + s->b);
+    s->tol1 = sqrt_eps * fabs(s->xf) + kXatol / 3.0;
+    s->tol2 = 2.0 * s->tol1;
+    if (s->num >= kMaxFun) {
+      s->flags |= kFlagBrentFail;  // scipy flag 1 -> res.success False
+      finished = true;
+    }
+  }
+  if (!finished && (fabs(s->xf - s->xm) > (s->tol2 - 0.5 * (s->b - s->a)))) {
+    // next trial point (loop body up to ``fu = func(x)``)
+    int golden = 1;
+    double x = s->xf;
+    if (fabs(s->e) > s->tol1) {
+      golden = 0;
+      double r = (s->xf - s->nfc) * (s->fx - s->ffulc);
+      double q = (s->xf - s->fulc) * (s->fx - s->fnfc);
+      double p = (s->xf - s->fulc) * q - (s->xf - s->nfc) * r;
+      q = 2.0 * (q - r);
+      if (q > 0.0) p = -p;
+      q = fabs(q);
+      r = s->e;
+      s->e = s->rat;
+      if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (s->a - s->xf)) &&
+          (p < q * (s->b - s->xf))) {
+        s->rat = (p + 0.0) / q;
+        x = s->xf + s->rat;
+        if (((x - s->a) < s->tol2) || ((s->b - x) < s->tol2)) {
+          double si = sgn(s->xm - s->xf) + ((s->xm - s->xf) == 0);
+          s->rat = s->tol1 * si;
+        }
+      } else {
+        golden = 1;
+      }
+    }
+    if (golden) {
+      if (s->xf >= s->xm)
+        s->e = s->a - s->xf;
+      else
+        s->e = s->b - s->xf;
+      s->rat = golden_mean * s->e;
+    }
+    double si = sgn(s->rat) + (s->rat == 0);
+    s->x = s->xf + si * fmax(fabs(s->rat), s->tol1);
+    s->phase = kNll;
+    return;
+  }
+  // Brent finished: qcml update
+  if (s->xf != s->xf || s->fx != s->fx || s->fu != s->fu)
+    s->flags |= kFlagBrentFail;
+  const double new_disp = s->xf / (1 - s->xf);
+  const double delta = fabs(s->disp - new_disp);
+  s->disp = new_disp;
+  s->qiter += 1;
+  if (delta > 1e-4 && !(delta < 1e-4) && s->qiter < 1000 &&
+      !(s->flags & kFlagBrentFail)) {
+    s->phase = kEqualize;
+    s->x = brent_x0();
+  } else {
+    if (s->qiter >= 1000 && delta > 1e-4) s->flags |= kFlagQcmlGuard;
+    s->phase = kDone;
+    s->result = s->disp;
+  }
+}
+
+}  // namespace h3d

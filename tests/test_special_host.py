@@ -1,0 +1,178 @@
+"""Host build of the device numerics (csrc/h3d_special.h, h3d_model.h) vs
+scipy / the oracle / reference goldens. CPU only: the same source the gfx950
+kernels compile, built with g++ (libh3d_hosttest.so)."""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.special as sc
+
+import oracle
+from conftest import golden, rel_err
+
+from hic3defdr_amd import build as h3dbuild
+
+D = ctypes.POINTER(ctypes.c_double)
+I = ctypes.POINTER(ctypes.c_int32)
+
+
+@pytest.fixture(scope='module')
+def lib():
+    return ctypes.CDLL(h3dbuild.build_hosttest())
+
+
+def _p(a, t=D):
+    return a.ctypes.data_as(t)
+
+
+def unary(lib, name, x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    getattr(lib, 'h3dt_' + name)(ctypes.c_int64(x.size), _p(x), _p(out))
+    return out
+
+
+def binary(lib, name, a, x):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    getattr(lib, 'h3dt_' + name)(ctypes.c_int64(x.size), _p(a), _p(x), _p(out))
+    return out
+
+
+def test_special_vs_reference_goldens(lib):
+    g = golden('unit_special.npz')
+    a, x, p = g['a'], g['x'], g['p']
+    assert rel_err(binary(lib, 'igam', a, x), g['gammainc']) < 1e-12
+    assert rel_err(binary(lib, 'igamc', a, x), g['gammaincc']) < 1e-12
+    assert rel_err(binary(lib, 'igami', a, p), g['gammaincinv']) < 1e-11
+    assert rel_err(binary(lib, 'igamci', a, p), g['gammainccinv']) < 1e-11
+    assert rel_err(unary(lib, 'ndtr', g['z']), g['ndtr']) < 1e-13
+    assert rel_err(unary(lib, 'ndtri', g['pq']), g['ndtri']) < 1e-13
+    assert rel_err(unary(lib, 'lgam', g['g']), g['gammaln']) < 1e-14
+    df1 = binary(lib, 'chi2_sf', np.ones_like(g['llr']), -2 * g['llr'])
+    df2 = binary(lib, 'chi2_sf', 2 * np.ones_like(g['llr']), -2 * g['llr'])
+    assert rel_err(df1, g['chi2_sf_df1']) < 1e-12
+    assert rel_err(df2, g['chi2_sf_df2']) < 1e-12
+
+
+def test_special_dense_grids(lib):
+    rng = np.random.default_rng(3)
+    # shapes/arguments met in q2qnbinom: a = mu/(1+alpha mu) in [1e-3, 2e3]
+    a = np.concatenate([10 ** rng.uniform(-3, 3.3, 20000)])
+    x = a * np.exp(rng.normal(0, 0.5, a.size))
+    assert rel_err(binary(lib, 'igam', a, x), sc.gammainc(a, x)) < 1e-12
+    assert rel_err(binary(lib, 'igamc', a, x), sc.gammaincc(a, x)) < 1e-12
+    q = np.clip(rng.uniform(0, 1, a.size) ** 4, 1e-300, 1 - 1e-16)
+    assert rel_err(binary(lib, 'igami', a, q), sc.gammaincinv(a, q)) < 1e-11
+    assert rel_err(binary(lib, 'igamci', a, q), sc.gammainccinv(a, q)) < 1e-11
+    z = rng.uniform(-37, 8, 20000)
+    assert rel_err(unary(lib, 'ndtr', z), sc.ndtr(z)) < 1e-13
+    pq = np.concatenate([10 ** rng.uniform(-307, -0.3, 20000),
+                         rng.uniform(0, 1, 20000)])
+    assert rel_err(unary(lib, 'ndtri', pq), sc.ndtri(pq)) < 1e-13
+    v = np.concatenate([10 ** rng.uniform(-3, 6, 20000),
+                        rng.uniform(0.01, 40, 20000)])
+    assert rel_err(unary(lib, 'lgam', v), sc.gammaln(v)) < 1e-14
+    s = rng.uniform(-0.49, 2, 5000)
+    # gammaln(1 + s) itself cancels near s = 0, 1: compare absolutely (the
+    # cephes Taylor series stops at n = 41: ~1e-14 at |s| = 0.5, as scipy)
+    assert np.max(np.abs(unary(lib, 'lgam1p', s) - sc.gammaln(1 + s))) < 5e-14
+
+
+def test_fit_mu_vs_goldens(lib):
+    g = golden('unit_nb.npz')
+    x = np.ascontiguousarray(g['fmh_x'], dtype=np.int32)
+    b = np.ascontiguousarray(g['fmh_b'])
+    for al, ref in ((g['fmh_alpha'], g['fmh_mu']),
+                    (np.full(b.shape, 0.05), g['fmh_mu_scalar_alpha'])):
+        al = np.ascontiguousarray(al)
+        mu = np.empty(len(x))
+        st = lib.h3dt_fit_mu(ctypes.c_int64(len(x)), 4, _p(x, I), _p(b),
+                             _p(al), _p(mu))
+        assert st == 0
+        assert rel_err(mu, ref) < 1e-9
+
+
+def test_fit_mu_doctest_brentq_case(lib):
+    """scaled_nb.py:129-137: the second pixel needs the brentq fallback."""
+    x = np.array([[2, 3, 4, 2], [6, 9, 3, 1]], dtype=np.int32)
+    b = np.array([[0.45, 0.53, 0.088, 0.091], [0.70, 0.83, 0.14, 0.15]])
+    al = np.array([[0.0071, 0.0071, 0.0073, 0.0073],
+                   [0.0070, 0.0070, 0.0072, 0.0072]])
+    mu = np.empty(2)
+    lib.h3dt_fit_mu(ctypes.c_int64(2), 4, _p(x, I), _p(b), _p(al), _p(mu))
+    np.testing.assert_allclose(mu, [9.5900971, 10.45962955], rtol=1e-8)
+
+
+def test_q2q_vs_goldens(lib):
+    g = golden('unit_nb.npz')
+    out = np.empty_like(g['q2q_x'])
+    lib.h3dt_q2q(ctypes.c_int64(out.size), _p(np.ascontiguousarray(g['q2q_x'])),
+                 _p(np.ascontiguousarray(g['q2q_mu_in'])),
+                 _p(np.ascontiguousarray(g['q2q_mu_out'])),
+                 _p(np.ascontiguousarray(g['q2q_alpha'])), _p(out))
+    # x = 0 with both means clamped maps to 0 +- 1e-17 rounding noise
+    np.testing.assert_allclose(out, g['q2q'], rtol=1e-10, atol=1e-12)
+
+
+def test_equalize_and_qcml_vs_goldens(lib):
+    g = golden('unit_nb.npz')
+    lib.h3dt_qcml.restype = ctypes.c_double
+    for s in range(int(g['n_segs'])):
+        data = np.ascontiguousarray(g['seg%d_data' % s], dtype=np.int32)
+        f = np.ascontiguousarray(g['seg%d_f' % s])
+        n, r = data.shape
+        out = np.empty((n, r))
+        st = lib.h3dt_equalize(ctypes.c_int64(n), r, _p(data, I), _p(f),
+                               ctypes.c_double(0.02), _p(out))
+        assert st == 0
+        np.testing.assert_allclose(out, g['seg%d_equalize' % s], rtol=1e-9,
+                                   atol=1e-12)
+        stat = ctypes.c_int(0)
+        q = lib.h3dt_qcml(ctypes.c_int64(n), r, _p(data, I), _p(f),
+                          ctypes.byref(stat))
+        assert stat.value == 0
+        np.testing.assert_allclose(q, g['seg%d_qcml' % s], rtol=1e-6,
+                                   atol=1e-10)
+
+
+def test_lrt_vs_goldens(lib):
+    g = golden('unit_nb.npz')
+    raw = np.ascontiguousarray(g['lrt_raw'], dtype=np.int32)
+    f = np.ascontiguousarray(g['lrt_f'])
+    disp = np.ascontiguousarray(g['lrt_disp'])
+    cor = np.ascontiguousarray(g['lrt_design'].argmax(axis=1), dtype=np.int32)
+    n = len(raw)
+    for pre, refit in (('lrt', 1), ('lrtnr', 0)):
+        p, llr, m0 = np.empty(n), np.empty(n), np.empty(n)
+        m1 = np.empty((n, 2))
+        st = lib.h3dt_lrt(ctypes.c_int64(n), 4, 2, _p(raw, I), _p(f), _p(disp),
+                          _p(cor, I), refit, _p(p), _p(llr), _p(m0), _p(m1))
+        assert st == 0
+        assert rel_err(p, g[pre + '_p']) < 1e-7
+        assert rel_err(m0, g[pre + '_mu0']) < 1e-9
+        assert rel_err(m1, g[pre + '_mu1']) < 1e-9
+
+
+def test_lrt_vs_oracle_r9c3(lib):
+    rng = np.random.default_rng(9)
+    n, R, C = 500, 9, 3
+    design = np.zeros((R, C), dtype=bool)
+    design[np.arange(R), np.arange(R) // 3] = True
+    mu = 10 ** rng.uniform(0, 2.5, n)
+    f = np.exp(rng.normal(0, 0.3, (n, R)))
+    disp = np.repeat(10 ** rng.uniform(-2, -0.5, (n, C)), 3, axis=1)
+    raw = rng.negative_binomial(1 / disp, 1 / (1 + disp * mu[:, None] * f))
+    for c in range(C):
+        raw[raw[:, design[:, c]].sum(axis=1) == 0, 3 * c] = 1
+    rp, rllr, rm0, rm1 = oracle.lrt(raw, f, disp, design)
+    raw32 = np.ascontiguousarray(raw, dtype=np.int32)
+    cor = np.ascontiguousarray(design.argmax(axis=1), dtype=np.int32)
+    p, llr, m0, m1 = np.empty(n), np.empty(n), np.empty(n), np.empty((n, C))
+    st = lib.h3dt_lrt(ctypes.c_int64(n), R, C, _p(raw32, I), _p(f),
+                      _p(np.ascontiguousarray(disp)), _p(cor, I), 1, _p(p),
+                      _p(llr), _p(m0), _p(m1))
+    assert st == 0
+    assert rel_err(p, rp) < 1e-7
+    assert rel_err(m1, rm1) < 1e-9
