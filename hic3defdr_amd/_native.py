@@ -1,0 +1,300 @@
+"""ctypes binding of libh3d.so (include/h3d.h).
+
+The product path has no CPU fallback: if the library or a gfx950 device is
+missing, every entry point raises ``H3DError``.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('H3D_LIB', os.path.join(PKG, 'lib', 'libh3d.so'))
+
+H3D_EST = {'qcml': 0, 'cml': 1, 'mme': 2}
+
+ERRORS = {-1: 'bad argument', -2: 'HIP runtime error',
+          -3: 'numerical failure', -4: 'out of device memory',
+          -5: 'invalid numeric input', -6: 'no gfx950 device'}
+
+EXPORTS = [
+    'h3d_version', 'h3d_device_count', 'h3d_open', 'h3d_close',
+    'h3d_last_error', 'h3d_set_stream', 'h3d_union_count', 'h3d_union_fill',
+    'h3d_size_factors_cmor', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
+    'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
+    'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
+]
+
+
+class H3DError(RuntimeError):
+    """A libh3d call failed (the reference would have raised too, or the
+    native library / GPU is unavailable)."""
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_D = ctypes.c_double
+ALLREDUCE_FN = ctypes.CFUNCTYPE(_I, ctypes.POINTER(_D), _I64, _P)
+
+_lib = None
+_lock = threading.RLock()  # context() -> Context() -> load_library()
+
+
+def load_library(path=None):
+    """Loads libh3d.so (once) and declares every prototype of h3d.h."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise H3DError('libh3d.so not found at %s: run '
+                           '`python -c "import __graft_entry__ as g; g.build()"`'
+                           % p)
+        lib = ctypes.CDLL(p)
+        sig = {
+            'h3d_version': (_I, []),
+            'h3d_device_count': (_I, []),
+            'h3d_open': (_P, [_I]),
+            'h3d_close': (None, [_P]),
+            'h3d_last_error': (ctypes.c_char_p, []),
+            'h3d_set_stream': (_I, [_P, _P]),
+            'h3d_union_count': (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
+            'h3d_union_fill': (_I, [_P, _P, _P, _P, _P, _I64]),
+            'h3d_size_factors_cmor': (_I, [_P, _P, _P, _I64, _I, _I, _P]),
+            'h3d_disp_per_dist': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I,
+                                       _I, _P, _P]),
+            'h3d_disp_per_dist_dev': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P,
+                                           _I, _I, _P, _P, ALLREDUCE_FN, _P]),
+            'h3d_disp_table': (_I, [_P, _I, _I, _D, _D, _P]),
+            'h3d_lrt': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I, _I, _P,
+                             _P, _P, _P, _P]),
+            'h3d_lrt_dev': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I, _I,
+                                 _P, _P, _P, _P, _P]),
+            'h3d_bh': (_I, [_P, _I64, _P]),
+            'h3d_profile_enable': (_I, [_P, _I]),
+            'h3d_profile_read': (_I, [_P, ctypes.c_char_p, _P, _P, _P]),
+            'h3d_profile_reset': (_I, [_P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = load_library().h3d_last_error().decode(errors='replace')
+        raise H3DError('%s: %s (%d: %s)' % (what, msg, rc,
+                                            ERRORS.get(rc, '?')))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class Context(object):
+    """One libh3d context bound to one GPU (``h3d_open``)."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = self.lib.h3d_open(device)
+        if not h:
+            raise H3DError('h3d_open(%d): %s' % (
+                device, self.lib.h3d_last_error().decode(errors='replace')))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.h3d_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle):
+        _check(self.lib.h3d_set_stream(self.handle, stream_handle),
+               'h3d_set_stream')
+
+    # -- prepare_data -------------------------------------------------------
+    def sparse_union(self, csrs, bias, dist_max):
+        """csrs: list of canonical scipy CSR (n_bins x n_bins); bias
+        (n_bins, R) filtered. Returns row, col (int32), raw (int64 (n, R)),
+        balanced (float64 (n, R))."""
+        R = len(csrs)
+        n_bins = bias.shape[0]
+        keep = []
+        ip = (ctypes.c_void_p * R)()
+        ix = (ctypes.c_void_p * R)()
+        dt = (ctypes.c_void_p * R)()
+        nnz = np.zeros(R, dtype=np.int64)
+        for r, m in enumerate(csrs):
+            a = _c(m.indptr, np.int64)
+            b = _c(m.indices, np.int32)
+            c = _c(m.data, np.float64)
+            keep += [a, b, c]
+            ip[r], ix[r], dt[r] = a.ctypes.data, b.ctypes.data, c.ctypes.data
+            nnz[r] = len(c)
+        bias = _c(bias, np.float64)
+        n_px = ctypes.c_int64(0)
+        _check(self.lib.h3d_union_count(
+            self.handle, R, n_bins, ip, ix, dt, _ptr(nnz), _ptr(bias),
+            int(dist_max), ctypes.byref(n_px)), 'h3d_union_count')
+        n = n_px.value
+        row = np.empty(n, dtype=np.int32)
+        col = np.empty(n, dtype=np.int32)
+        raw = np.empty((n, R), dtype=np.int64)
+        bal = np.empty((n, R), dtype=np.float64)
+        _check(self.lib.h3d_union_fill(self.handle, _ptr(row), _ptr(col),
+                                       _ptr(raw), _ptr(bal), n),
+               'h3d_union_fill')
+        return row, col, raw, bal
+
+    def size_factors_cmor(self, balanced, dist, n_bins):
+        balanced = _c(balanced, np.float64)
+        dist = _c(dist, np.int32)
+        n, R = balanced.shape
+        out = np.empty((n, R), dtype=np.float64)
+        _check(self.lib.h3d_size_factors_cmor(
+            self.handle, _ptr(balanced), _ptr(dist), n, R,
+            int(n_bins or 0), _ptr(out)), 'h3d_size_factors_cmor')
+        return out
+
+    # -- estimate_disp ------------------------------------------------------
+    def disp_per_dist(self, raw, f, dist, cond_of_rep, C, D,
+                      estimator='qcml'):
+        raw = _c(raw, np.int64)
+        f = _c(f, np.float64)
+        dist = _c(dist, np.int32)
+        cond = _c(cond_of_rep, np.int32)
+        n, R = raw.shape
+        out = np.empty((D, C), dtype=np.float64)
+        flags = np.zeros((D, C), dtype=np.int32)
+        _check(self.lib.h3d_disp_per_dist(
+            self.handle, _ptr(raw), _ptr(f), _ptr(dist), n, R, C, _ptr(cond),
+            D, H3D_EST[estimator], _ptr(out), _ptr(flags)),
+            'h3d_disp_per_dist')
+        return out
+
+    def disp_per_dist_dev(self, d_raw, d_f, d_dist, n, R, cond_of_rep, C, D,
+                          reduce=None):
+        """Device-pointer variant; ``reduce(ptr, count)`` all-reduces a device
+        buffer of doubles in place (multi-GPU)."""
+        cond = _c(cond_of_rep, np.int32)
+        out = np.empty((D, C), dtype=np.float64)
+        flags = np.zeros((D, C), dtype=np.int32)
+        if reduce is not None:
+            def _cb(ptr, count, user):
+                try:
+                    reduce(ctypes.cast(ptr, ctypes.c_void_p).value, count)
+                    return 0
+                except Exception:  # surfaced as H3D_EHIP by the library
+                    return 1
+            cb = ALLREDUCE_FN(_cb)
+        else:
+            cb = ALLREDUCE_FN()
+        _check(self.lib.h3d_disp_per_dist_dev(
+            self.handle, d_raw, d_f, d_dist, n, R, C, _ptr(cond), D, 0,
+            _ptr(out), _ptr(flags), cb, None), 'h3d_disp_per_dist_dev')
+        return out
+
+    # -- lrt -----------------------------------------------------------------
+    def lrt(self, raw, f, dist, disp_table, cond_of_rep, refit_mu=True,
+            want_disp=True):
+        """``dist=None``: ``disp_table`` is the per-pixel dispersion (n, C)."""
+        raw = _c(raw, np.int64)
+        f = _c(f, np.float64)
+        dist = _c(dist, np.int32) if dist is not None else None
+        tab = _c(disp_table, np.float64)
+        cond = _c(cond_of_rep, np.int32)
+        n, R = raw.shape
+        D, C = tab.shape
+        if dist is None:
+            if D != n:
+                raise ValueError('per-pixel disp must be (n, C)')
+            D = 0
+        p = np.empty(n)
+        llr = np.empty(n)
+        mu0 = np.empty(n)
+        mu1 = np.empty((n, C))
+        disp = np.empty((n, C)) if want_disp else None
+        _check(self.lib.h3d_lrt(
+            self.handle, _ptr(raw), _ptr(f), _ptr(dist), _ptr(tab), n, R, C,
+            _ptr(cond), D, int(bool(refit_mu)), _ptr(p), _ptr(llr), _ptr(mu0),
+            _ptr(mu1), _ptr(disp)), 'h3d_lrt')
+        return p, llr, mu0, mu1, disp
+
+    def lrt_dev(self, d_raw, d_f, d_dist, disp_table, n, R, cond_of_rep,
+                d_p, d_llr, d_mu0, d_mu1, d_disp=None, refit_mu=True):
+        tab = _c(disp_table, np.float64)
+        cond = _c(cond_of_rep, np.int32)
+        D, C = tab.shape
+        _check(self.lib.h3d_lrt_dev(
+            self.handle, d_raw, d_f, d_dist, _ptr(tab), n, R, C, _ptr(cond),
+            D, int(bool(refit_mu)), d_p, d_llr, d_mu0, d_mu1, d_disp),
+            'h3d_lrt_dev')
+
+    # -- measurement ---------------------------------------------------------
+    def profile(self, on=True):
+        _check(self.lib.h3d_profile_enable(self.handle, int(on)),
+               'h3d_profile_enable')
+
+    def profile_reset(self):
+        _check(self.lib.h3d_profile_reset(self.handle), 'h3d_profile_reset')
+
+    def profile_read(self, name):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        u = ctypes.c_int64(0)
+        _check(self.lib.h3d_profile_read(self.handle, name.encode(),
+                                         ctypes.byref(ms), ctypes.byref(n),
+                                         ctypes.byref(u)), 'h3d_profile_read')
+        return ms.value, n.value, u.value
+
+
+def disp_table(disp_per_dist_col, weighted=True, frac=None,
+               auto_frac_factor=15.):
+    """Host-side smoother (libh3d, C++): the fitted dispersion function
+    tabulated at every integer distance."""
+    lib = load_library()
+    col = _c(disp_per_dist_col, np.float64)
+    out = np.empty(len(col))
+    _check(lib.h3d_disp_table(_ptr(col), len(col), int(bool(weighted)),
+                              -1.0 if frac is None else float(frac),
+                              float(auto_frac_factor), _ptr(out)),
+           'h3d_disp_table')
+    return out
+
+
+def bh(pvalues):
+    lib = load_library()
+    p = _c(pvalues, np.float64)
+    q = np.empty_like(p)
+    _check(lib.h3d_bh(_ptr(p), len(p), _ptr(q)), 'h3d_bh')
+    return q
+
+
+_ctx = {}
+
+
+def context(device=None):
+    """Process-wide context for ``device`` (default: LOCAL_RANK or 0)."""
+    if device is None:
+        device = int(os.environ.get('LOCAL_RANK', '0'))
+    with _lock:
+        if device not in _ctx:
+            _ctx[device] = Context(device)
+        return _ctx[device]

@@ -1,0 +1,199 @@
+"""Pipeline mixin (reference hic3defdr/analysis/analysis.py:24-364).
+
+Same methods, signatures and outdir outputs as the reference; the per-pixel
+work runs on the GPU through libh3d.so:
+
+  prepare_data  -> h3d_union_count/fill (union + raw/balanced gathers),
+                   h3d_size_factors_cmor (conditional median of ratios)
+  estimate_disp -> h3d_disp_per_dist (qcml per distance x condition),
+                   h3d_disp_table (lowess smoother, host C++ in libh3d)
+  lrt           -> h3d_lrt (fused per-pixel NB GLM fits + LRT + chi2)
+  bh            -> h3d_bh
+
+``n_threads`` is accepted for signature compatibility: the reference's
+process pools (util/parallelization.py) are replaced by the GPU; multi-GPU
+sharding is hic3defdr_amd.parallel.
+"""
+import numpy as np
+import scipy.sparse as sparse
+
+from hic3defdr_amd import _native
+from hic3defdr_amd.analysis.core import DispFn
+from hic3defdr_amd.util.clusters import load_clusters, pixel_membership
+from hic3defdr_amd.util.printing import eprint
+
+NATIVE_NORMS = ('conditional_mor',)
+NATIVE_ESTIMATORS = ('qcml',)
+
+
+def _canonical_csr(fname):
+    m = sparse.load_npz(fname).tocsr()
+    m.sum_duplicates()  # sorted, duplicate-free rows (what the kernels expect)
+    return m
+
+
+class AnalyzingHiC3DeFDR(object):
+
+    def _ctx(self):
+        return _native.context()
+
+    def _cond_of_rep(self):
+        d = np.asarray(self.design, dtype=bool)
+        if not np.all(d.sum(axis=1) == 1):
+            raise ValueError('every replicate must belong to exactly one '
+                             'condition')
+        return d.argmax(axis=1).astype(np.int32)
+
+    # ------------------------------------------------------------------
+    def prepare_data(self, chrom=None, norm='conditional_mor', n_bins=-1,
+                     n_threads=-1, verbose=True):
+        """Reference ``analysis.py:28-133``."""
+        if n_bins == -1:
+            n_bins = int(self.dist_thresh_max / 5)
+        if chrom is None:
+            for c in self.chroms:
+                self.prepare_data(chrom=c, norm=norm, n_bins=n_bins,
+                                  verbose=verbose)
+            return
+        if norm not in NATIVE_NORMS:
+            raise NotImplementedError(
+                'norm=%r: the GPU path implements %s' % (norm, NATIVE_NORMS))
+        eprint('preparing data for chrom %s' % chrom, skip=not verbose)
+        bias = self.load_bias(chrom)
+        mats = [_canonical_csr(p.replace('<chrom>', chrom))
+                for p in self.raw_npz_patterns]
+        ctx = self._ctx()
+        eprint('  computing union pixel set', skip=not verbose)
+        row, col, raw, balanced = ctx.sparse_union(mats, bias,
+                                                   self.dist_thresh_max)
+        eprint('  computing size factors', skip=not verbose)
+        dist = col - row
+        size_factors = ctx.size_factors_cmor(balanced, dist, n_bins or 0)
+        scaled = balanced / size_factors
+        design = np.asarray(self.design, dtype=bool)
+        mean = np.dot(scaled, design) / np.sum(design, axis=0)
+        disp_idx = np.all(mean >= self.mean_thresh, axis=1) & \
+            (dist >= self.dist_thresh_min)
+        if self.loop_patterns:
+            eprint('  making loop_idx', skip=not verbose)
+            cl = [load_clusters(p.replace('<chrom>', chrom))
+                  for p in self.loop_patterns.values()]
+            loop_idx = pixel_membership(row[disp_idx], col[disp_idx], cl)
+            self.save_data(loop_idx, 'loop_idx', chrom)
+        eprint('  saving data to disk', skip=not verbose)
+        self.save_data(row, 'row', chrom)
+        self.save_data(col, 'col', chrom)
+        self.save_data(raw, 'raw', chrom)
+        self.save_data(size_factors, 'size_factors', chrom)
+        self.save_data(scaled, 'scaled', chrom)
+        self.save_data(disp_idx, 'disp_idx', chrom)
+
+    # ------------------------------------------------------------------
+    def _f_and_dist(self):
+        """raw/f/dist of the disp pixels, all chromosomes concatenated
+        (reference ``analysis.py:169-183``)."""
+        disp_idx, disp_idx_offsets = self.load_data('disp_idx', 'all')
+        row, offsets = self.load_data('row', 'all', idx=disp_idx)
+        col, _ = self.load_data('col', 'all', idx=disp_idx)
+        raw, _ = self.load_data('raw', 'all', idx=disp_idx)
+        dist = col - row
+        f = np.ones_like(raw, dtype=float)
+        for i, chrom in enumerate(self.chroms):
+            sl = slice(offsets[i], offsets[i + 1])
+            di = disp_idx[disp_idx_offsets[i]:disp_idx_offsets[i + 1]]
+            bias = self.load_bias(chrom)
+            sf = self.load_data('size_factors', chrom)[di]
+            f[sl] = bias[row[sl], :] * bias[col[sl], :] * sf
+        return raw, f, dist, offsets
+
+    def estimate_disp(self, estimator='qcml', frac=None, auto_frac_factor=15.,
+                      weighted_lowess=True, n_threads=-1):
+        """Reference ``analysis.py:135-223``."""
+        eprint('estimating dispersion')
+        raw, f, dist, offsets = self._f_and_dist()
+        design = np.asarray(self.design, dtype=bool)
+        C = design.shape[1]
+        D = self.dist_thresh_max + 1
+        if callable(estimator):
+            # a user-supplied Python estimator runs where the user wrote it
+            disp_per_dist = np.zeros((D, C))
+            for c in range(C):
+                for d in range(D):
+                    sel = dist == d
+                    rs = raw[sel][:, design[:, c]]
+                    fs = f[sel][:, design[:, c]]
+                    disp_per_dist[d, c] = np.nan if not rs.size else \
+                        estimator(rs, f=fs)
+        elif estimator in NATIVE_ESTIMATORS:
+            disp_per_dist = self._ctx().disp_per_dist(
+                raw, f, dist, self._cond_of_rep(), C, D, estimator=estimator)
+        else:
+            raise NotImplementedError(
+                'estimator=%r: the reference divides its int64 raw slice in '
+                'place for cml/mme (dispersion.py:76,129) and raises; the GPU '
+                'path implements %s' % (estimator, NATIVE_ESTIMATORS))
+        disp = np.zeros((len(raw), C))
+        for c, cond in enumerate(self.design.columns):
+            eprint('  fitting distance vs dispersion relationship')
+            table = _native.disp_table(disp_per_dist[:, c],
+                                       weighted=weighted_lowess, frac=frac,
+                                       auto_frac_factor=auto_frac_factor)
+            fn = DispFn(table, disp_per_dist[:, c], weighted=weighted_lowess)
+            disp[:, c] = table[dist]
+            self.save_disp_fn(cond, fn)
+        eprint('  saving estimated dispersions to disk')
+        self.save_data(disp, 'disp', offsets)
+        self.save_data(disp_per_dist, 'disp_per_dist')
+
+    # ------------------------------------------------------------------
+    def lrt(self, chrom=None, refit_mu=True, n_threads=-1, verbose=True):
+        """Reference ``analysis.py:225-284``."""
+        if chrom is None:
+            for c in self.chroms:
+                self.lrt(chrom=c, refit_mu=refit_mu, verbose=verbose)
+            return
+        eprint('running LRT for chrom %s' % chrom, skip=not verbose)
+        bias = self.load_bias(chrom)
+        size_factors = self.load_data('size_factors', chrom)
+        disp_idx = self.load_data('disp_idx', chrom)
+        row = self.load_data('row', chrom, idx=disp_idx)
+        col = self.load_data('col', chrom, idx=disp_idx)
+        raw = self.load_data('raw', chrom, idx=disp_idx)
+        disp = self.load_data('disp', chrom)
+        if len(size_factors.shape) == 2:
+            f = bias[row] * bias[col] * size_factors[disp_idx, :]
+        else:
+            f = bias[row] * bias[col] * size_factors
+        p, llr, mu0, mu1, _ = self._ctx().lrt(raw, f, None, disp,
+                                              self._cond_of_rep(),
+                                              refit_mu=refit_mu,
+                                              want_disp=False)
+        self.save_data(p, 'pvalues', chrom)
+        self.save_data(llr, 'llr', chrom)
+        self.save_data(mu0, 'mu_hat_null', chrom)
+        self.save_data(mu1, 'mu_hat_alt', chrom)
+
+    # ------------------------------------------------------------------
+    def bh(self):
+        """Reference ``analysis.py:286-303``."""
+        eprint('applying BH-FDR correction')
+        loop_idx = self.load_data('loop_idx', 'all')[0] \
+            if self.loop_patterns else None
+        pvalues, offsets = self.load_data('pvalues', 'all', idx=loop_idx)
+        q = _native.bh(pvalues)
+        for i, chrom in enumerate(self.chroms):
+            self.save_data(q[offsets[i]:offsets[i + 1]], 'qvalues', chrom)
+
+    def run_to_qvalues(self, norm='conditional_mor', n_bins_norm=-1,
+                       estimator='qcml', frac=None, auto_frac_factor=15.,
+                       weighted_lowess=True, refit_mu=True, n_threads=-1,
+                       verbose=True):
+        """Reference ``analysis.py:305-364``."""
+        self.prepare_data(norm=norm, n_bins=n_bins_norm, n_threads=n_threads,
+                          verbose=verbose)
+        self.estimate_disp(estimator=estimator, frac=frac,
+                           auto_frac_factor=auto_frac_factor,
+                           weighted_lowess=weighted_lowess,
+                           n_threads=n_threads)
+        self.lrt(refit_mu=refit_mu, n_threads=n_threads, verbose=verbose)
+        self.bh()

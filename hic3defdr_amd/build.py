@@ -20,7 +20,8 @@ HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 
 NATIVE_SRCS = ['h3d_api.hip']
-HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h']
+HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
+           'h3d_prepare.h', 'h3d_prepare_api.h']
 
 
 def _stale(target, deps):

@@ -1,0 +1,633 @@
+// libh3d.so: C ABI (include/h3d.h) + orchestration of the gfx950 kernels.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "h3d.h"
+#include "h3d_host.h"
+#include "h3d_kernels.h"
+#include "h3d_prepare.h"
+
+using namespace h3d;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                      \
+  do {                                                                     \
+    hipError_t e_ = (expr);                                                \
+    if (e_ != hipSuccess)                                                  \
+      return fail(H3D_EHIP, "%s failed: %s (%s:%d)", #expr,                \
+                  hipGetErrorString(e_), __FILE__, __LINE__);              \
+  } while (0)
+
+struct ProfEntry {
+  double ms = 0.0;
+  int64_t launches = 0;
+  int64_t units = 0;
+};
+
+}  // namespace
+
+struct h3d_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int n_cu = 256;
+  bool prof = false;
+  std::map<std::string, ProfEntry> stats;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<int64_t> pending_units;
+  std::vector<hipEvent_t> event_pool;
+  // grow-only device scratch, by slot
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  // prepare_data state between h3d_union_count and h3d_union_fill
+  PrepUnion prep;
+};
+
+namespace {
+
+void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes) {
+  auto& b = ctx->bufs[slot];
+  if (b.second >= bytes && b.first) return b.first;
+  if (b.first) (void)hipFree(b.first);
+  b.first = nullptr;
+  b.second = 0;
+  void* p = nullptr;
+  if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
+  b.first = p;
+  b.second = std::max<size_t>(bytes, 256);
+  return p;
+}
+
+hipEvent_t ev_get(h3d_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// wraps one kernel launch with HIP events on the ctx stream when profiling
+struct ProfScope {
+  h3d_ctx* ctx;
+  const char* name;
+  int64_t units;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(h3d_ctx* c, const char* n, int64_t u) : ctx(c), name(n), units(u) {
+    if (ctx->prof) {
+      a = ev_get(ctx);
+      b = ev_get(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~ProfScope() {
+    if (ctx->prof) {
+      (void)hipEventRecord(b, ctx->stream);
+      ctx->pending.push_back({name, {a, b}});
+      ctx->pending_units.push_back(units);
+    }
+  }
+};
+
+void prof_collect(h3d_ctx* ctx) {
+  if (ctx->pending.empty()) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  for (size_t i = 0; i < ctx->pending.size(); ++i) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ctx->pending[i].second.first,
+                              ctx->pending[i].second.second);
+    auto& e = ctx->stats[ctx->pending[i].first];
+    e.ms += ms;
+    e.launches += 1;
+    e.units += ctx->pending_units[i];
+    ctx->event_pool.push_back(ctx->pending[i].second.first);
+    ctx->event_pool.push_back(ctx->pending[i].second.second);
+  }
+  ctx->pending.clear();
+  ctx->pending_units.clear();
+}
+
+int grid_for(h3d_ctx* ctx, int64_t n, int per_cu = 8) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  g = std::min<int64_t>(g, (int64_t)ctx->n_cu * per_cu);
+  return (int)std::max<int64_t>(g, 1);
+}
+
+int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
+               std::vector<int32_t>* rep_idx) {
+  if (R < 1 || R > kMaxReps) return fail(H3D_EARG, "R=%d outside [1, %d]", R, kMaxReps);
+  if (C < 1 || C > kMaxConds) return fail(H3D_EARG, "C=%d outside [1, %d]", C, kMaxConds);
+  nrep->assign(C, 0);
+  rep_idx->assign((size_t)C * kMaxReps, 0);
+  for (int r = 0; r < R; ++r) {
+    const int c = cond_of_rep[r];
+    if (c < 0 || c >= C) return fail(H3D_EARG, "cond_of_rep[%d]=%d", r, c);
+    (*rep_idx)[(size_t)c * kMaxReps + (*nrep)[c]] = r;
+    (*nrep)[c] += 1;
+  }
+  for (int c = 0; c < C; ++c)
+    if ((*nrep)[c] == 0) return fail(H3D_EARG, "condition %d has no replicates", c);
+  return 0;
+}
+
+template <int M>
+void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
+                      const double* f_s, double* pd, int64_t n,
+                      const int64_t* cs, const int32_t* cl, const int32_t* cd,
+                      int C, const int32_t* rep_idx, const int32_t* n_rep,
+                      const SegState* st, int* seg_flags, const int32_t* list,
+                      const int32_t* list_len, double* partial) {
+  hipLaunchKernelGGL(k_disp_work<M>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                     raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
+                     seg_flags, list, list_len, partial);
+}
+
+template <int M, int CM>
+void launch_lrt(h3d_ctx* ctx, int grid, const int32_t* raw, const double* f,
+                const int32_t* dist, const double* table, int64_t n, int R,
+                int C, int D, const int32_t* cond, int refit, double* p,
+                double* llr, double* mu0, double* mu1, double* disp,
+                int* flags) {
+  hipLaunchKernelGGL((k_lrt<M, CM>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                     raw, f, dist, table, n, R, C, D, cond, refit, p, llr, mu0,
+                     mu1, disp, flags);
+}
+
+int flags_to_code(int fl) {
+  if (fl & kFlagBadInput) return fail(H3D_EINPUT, "non-positive or non-finite dispersion / scaling factor (status %d)", fl);
+  if (fl & (kFlagNoRoot | kFlagNoConv)) return fail(H3D_ENOCONV, "mean MLE failed (status %d)", fl);
+  if (fl & (kFlagBrentFail | kFlagQcmlGuard)) return fail(H3D_ENOCONV, "dispersion optimisation failed (status %d)", fl);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int h3d_version(void) { return 1; }
+
+const char* h3d_last_error(void) { return g_err.c_str(); }
+
+int h3d_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+h3d_ctx* h3d_open(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    fail(H3D_ENODEV, "no HIP device visible");
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    fail(H3D_EARG, "device %d of %d", device, n);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    fail(H3D_EHIP, "hipGetDeviceProperties failed");
+    return nullptr;
+  }
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fail(H3D_ENODEV, "device %d is %s, libh3d is built for gfx950", device,
+         prop.gcnArchName);
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail(H3D_EHIP, "hipSetDevice failed");
+    return nullptr;
+  }
+  h3d_ctx* ctx = new h3d_ctx();
+  ctx->device = device;
+  ctx->n_cu = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    fail(H3D_EHIP, "stream create failed");
+    return nullptr;
+  }
+  ctx->stream = ctx->own;
+  return ctx;
+}
+
+void h3d_close(h3d_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  prof_collect(ctx);
+  for (auto& kv : ctx->bufs)
+    if (kv.second.first) (void)hipFree(kv.second.first);
+  for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+}
+
+int h3d_set_stream(h3d_ctx* ctx, void* stream) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  ctx->stream = stream ? (hipStream_t)stream : ctx->own;
+  return 0;
+}
+
+int h3d_profile_enable(h3d_ctx* ctx, int on) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  prof_collect(ctx);
+  ctx->prof = on != 0;
+  return 0;
+}
+
+int h3d_profile_reset(h3d_ctx* ctx) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  prof_collect(ctx);
+  ctx->stats.clear();
+  return 0;
+}
+
+int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
+                     int64_t* launches, int64_t* units) {
+  if (!ctx || !name) return fail(H3D_EARG, "null argument");
+  prof_collect(ctx);
+  auto it = ctx->stats.find(name);
+  ProfEntry e = (it == ctx->stats.end()) ? ProfEntry() : it->second;
+  if (total_ms) *total_ms = e.ms;
+  if (launches) *launches = e.launches;
+  if (units) *units = e.units;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// estimate_disp
+// ---------------------------------------------------------------------------
+
+int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                          const int32_t* d_dist, int64_t n, int R, int C,
+                          const int32_t* cond_of_rep, int D, int estimator,
+                          double* disp_per_dist, int32_t* seg_flags_out,
+                          h3d_allreduce_fn reduce, void* user) {
+  if (!ctx || !cond_of_rep || !disp_per_dist) return fail(H3D_EARG, "null argument");
+  if (n < 0 || D < 1) return fail(H3D_EARG, "n=%lld D=%d", (long long)n, D);
+  if (n > 0 && (!d_raw || !d_f || !d_dist)) return fail(H3D_EARG, "null device input");
+  if (n >= (int64_t)1 << 31) return fail(H3D_EARG, "n=%lld exceeds 2^31 pixels per call", (long long)n);
+  if (estimator != H3D_EST_QCML)
+    return fail(H3D_EARG, "estimator %d: only qcml runs on the GPU path (the reference's cml/mme divide an int64 array in place and raise)", estimator);
+  std::vector<int> nrep;
+  std::vector<int32_t> rep_idx;
+  if (int rc = check_cond(cond_of_rep, R, C, &nrep, &rep_idx)) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int S = D * C;
+  const int maxnr = *std::max_element(nrep.begin(), nrep.end());
+
+  // 1. stable sort of the pixels by distance, SoA gather
+  std::vector<int64_t> seg_start(D + 1, 0);
+  int32_t *raw_s = nullptr, *dist_s = nullptr;
+  double *f_s = nullptr, *pd = nullptr;
+  if (n > 0) {
+    ProfScope ps(ctx, "disp_prep", n);
+    int32_t* idx_in = (int32_t*)scratch(ctx, "idx_in", n * 4);
+    int32_t* idx_out = (int32_t*)scratch(ctx, "idx_out", n * 4);
+    dist_s = (int32_t*)scratch(ctx, "dist_s", n * 4);
+    raw_s = (int32_t*)scratch(ctx, "raw_s", n * R * 4);
+    f_s = (double*)scratch(ctx, "f_s", n * R * 8);
+    pd = (double*)scratch(ctx, "pd", n * R * 8);
+    int64_t* d_seg = (int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
+    if (!idx_in || !idx_out || !dist_s || !raw_s || !f_s || !pd || !d_seg)
+      return fail(H3D_ENOMEM, "device allocation failed (n=%lld)", (long long)n);
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, idx_in, n);
+    int end_bit = 1;
+    while ((1 << end_bit) <= D) ++end_bit;
+    size_t tmp_bytes = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_dist, dist_s,
+                                               idx_in, idx_out, (int)n, 0, end_bit, s));
+    void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+    if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
+                                               idx_out, (int)n, 0, end_bit, s));
+    hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                       idx_out, d_raw, d_f, n, R, raw_s, f_s);
+    hipLaunchKernelGGL(k_seg_bounds, dim3((D + 1 + 255) / 256), dim3(256), 0, s,
+                       dist_s, n, D, d_seg);
+    HIP_TRY(hipMemcpyAsync(seg_start.data(), d_seg, (D + 1) * 8,
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (seg_start[0] != 0 || seg_start[D] != n) {
+      // pixels with dist < 0 or >= D
+      return fail(H3D_EARG, "dist outside [0, %d)", D);
+    }
+  }
+
+  // 2. chunk table
+  std::vector<int64_t> cs;
+  std::vector<int32_t> cl, cd, scb(D), sce(D);
+  for (int d = 0; d < D; ++d) {
+    scb[d] = (int32_t)cl.size();
+    for (int64_t a = seg_start[d]; a < seg_start[d + 1]; a += kChunk) {
+      cs.push_back(a);
+      cl.push_back((int32_t)std::min<int64_t>(kChunk, seg_start[d + 1] - a));
+      cd.push_back(d);
+    }
+    sce[d] = (int32_t)cl.size();
+  }
+  const int n_chunks = (int)cl.size();
+
+  // global pixel counts per segment (all ranks)
+  std::vector<double> cnt(S, 0.0);
+  for (int d = 0; d < D; ++d)
+    for (int c = 0; c < C; ++c) cnt[d * C + c] = (double)(seg_start[d + 1] - seg_start[d]);
+  double* d_cnt = (double*)scratch(ctx, "seg_cnt", S * 8);
+  if (!d_cnt) return fail(H3D_ENOMEM, "seg_cnt");
+  if (reduce) {
+    HIP_TRY(hipMemcpyAsync(d_cnt, cnt.data(), S * 8, hipMemcpyHostToDevice, s));
+    if (reduce(d_cnt, S, user)) return fail(H3D_EHIP, "allreduce callback failed");
+    HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+
+  std::vector<SegState> st(S);
+  for (int sg = 0; sg < S; ++sg) seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C]);
+
+  auto up = [&](const char* slot, const void* src, size_t bytes) -> void* {
+    void* p = scratch(ctx, slot, bytes);
+    if (p && bytes) (void)hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, s);
+    return p;
+  };
+  int64_t* d_cs = (int64_t*)up("chunk_start", cs.data(), cs.size() * 8);
+  int32_t* d_cl = (int32_t*)up("chunk_len", cl.data(), cl.size() * 4);
+  int32_t* d_cd = (int32_t*)up("chunk_d", cd.data(), cd.size() * 4);
+  int32_t* d_scb = (int32_t*)up("seg_chunk_b", scb.data(), D * 4);
+  int32_t* d_sce = (int32_t*)up("seg_chunk_e", sce.data(), D * 4);
+  std::vector<int32_t> nrep32(nrep.begin(), nrep.end());
+  int32_t* d_nrep = (int32_t*)up("n_rep", nrep32.data(), C * 4);
+  int32_t* d_repidx = (int32_t*)up("rep_idx", rep_idx.data(), rep_idx.size() * 4);
+  SegState* d_st = (SegState*)up("seg_state", st.data(), S * sizeof(SegState));
+  const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
+  int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
+  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // list_len, active
+  int32_t* d_slb = (int32_t*)scratch(ctx, "seg_lb", S * 4);
+  int32_t* d_sle = (int32_t*)scratch(ctx, "seg_le", S * 4);
+  double* d_partial = (double*)scratch(ctx, "partial", max_items * 8);
+  double* d_total = (double*)scratch(ctx, "seg_total", S * 8);
+  int* d_flags = (int*)scratch(ctx, "seg_flags", S * 4);
+  double* d_res = (double*)scratch(ctx, "seg_result", S * 8);
+  if (!d_cs || !d_cl || !d_cd || !d_scb || !d_sce || !d_nrep || !d_repidx ||
+      !d_st || !d_list || !d_meta || !d_slb || !d_sle || !d_partial ||
+      !d_total || !d_flags || !d_res)
+    return fail(H3D_ENOMEM, "disp scratch");
+  HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));
+
+  // initial active list
+  hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
+                     d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_meta, d_slb,
+                     d_sle, d_res, d_meta + 1, 1);
+  const int work_grid = std::max(1, std::min<int>((int)max_items, ctx->n_cu * 4));
+  int32_t* h_meta = nullptr;
+  HIP_TRY(hipHostMalloc((void**)&h_meta, 16, hipHostMallocDefault));
+  int rounds = 0, batch = 2, rc = 0;
+  while (true) {
+    for (int b = 0; b < batch; ++b) {
+      {
+        ProfScope ps(ctx, "disp_work", 0);
+        switch (maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32) {
+          case 4:
+            launch_disp_work<4>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            break;
+          case 8:
+            launch_disp_work<8>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            break;
+          case 16:
+            launch_disp_work<16>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            break;
+          default:
+            launch_disp_work<32>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+        }
+      }
+      {
+        ProfScope ps(ctx, "disp_reduce", 0);
+        hipLaunchKernelGGL(k_seg_reduce, dim3((S + 3) / 4), dim3(256), 0, s,
+                           d_partial, d_slb, d_sle, S, d_total);
+      }
+      if (reduce && reduce(d_total, S, user)) {
+        rc = fail(H3D_EHIP, "allreduce callback failed");
+        break;
+      }
+      {
+        ProfScope ps(ctx, "disp_update", 0);
+        hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
+                           d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_meta,
+                           d_slb, d_sle, d_res, d_meta + 1, 0);
+      }
+      ++rounds;
+    }
+    if (rc) break;
+    if (hipMemcpyAsync(h_meta, d_meta, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(hipGetLastError()));
+      break;
+    }
+    if (std::getenv("H3D_DEBUG"))
+      fprintf(stderr, "[h3d] disp rounds=%d active_items=%d\n", rounds, h_meta[1]);
+    if (h_meta[1] == 0) break;
+    if (rounds > 200000) {
+      rc = fail(H3D_ENOCONV, "estimate_disp did not terminate");
+      break;
+    }
+    batch = std::min(batch * 2, 8);
+  }
+  (void)hipHostFree(h_meta);
+  if (rc) return rc;
+  prof_collect(ctx);
+  std::vector<int32_t> fl(S);
+  HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(st.data(), d_st, S * sizeof(SegState), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  int all = 0;
+  for (int sg = 0; sg < S; ++sg) {
+    fl[sg] = st[sg].flags;
+    all |= fl[sg];
+  }
+  if (seg_flags_out) std::memcpy(seg_flags_out, fl.data(), S * 4);
+  return flags_to_code(all);
+}
+
+int h3d_disp_per_dist(h3d_ctx* ctx, const int64_t* raw, const double* f,
+                      const int32_t* dist, int64_t n, int R, int C,
+                      const int32_t* cond_of_rep, int D, int estimator,
+                      double* disp_per_dist, int32_t* seg_flags) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  if (n > 0 && (!raw || !f || !dist)) return fail(H3D_EARG, "null input");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  int32_t* d_raw = nullptr;
+  double* d_f = nullptr;
+  int32_t* d_dist = nullptr;
+  if (n > 0) {
+    int64_t* d_raw64 = (int64_t*)scratch(ctx, "in_raw64", n * R * 8);
+    d_raw = (int32_t*)scratch(ctx, "in_raw", n * R * 4);
+    d_f = (double*)scratch(ctx, "in_f", n * R * 8);
+    d_dist = (int32_t*)scratch(ctx, "in_dist", n * 4);
+    int* d_ovf = (int*)scratch(ctx, "ovf", 4);
+    if (!d_raw64 || !d_raw || !d_f || !d_dist || !d_ovf) return fail(H3D_ENOMEM, "inputs");
+    HIP_TRY(hipMemcpyAsync(d_raw64, raw, n * R * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_f, f, n * R * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_ovf, 0, 4, s));
+    hipLaunchKernelGGL(k_i64_to_i32, dim3(grid_for(ctx, n * R)), dim3(kBlock), 0, s,
+                       d_raw64, d_raw, n * R, d_ovf);
+    int ovf = 0;
+    HIP_TRY(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ovf) return fail(H3D_EINPUT, "raw counts must be in [0, 2^31)");
+  }
+  return h3d_disp_per_dist_dev(ctx, d_raw, d_f, d_dist, n, R, C, cond_of_rep, D,
+                               estimator, disp_per_dist, seg_flags, nullptr, nullptr);
+}
+
+int h3d_disp_table(const double* col, int D, int weighted, double frac,
+                   double auto_frac_factor, double* table_out) {
+  if (!col || !table_out || D < 1) return fail(H3D_EARG, "null argument / D");
+  std::vector<double> x, y, xs(D);
+  for (int d = 0; d < D; ++d) {
+    xs[d] = d;
+    if (std::isfinite(col[d])) {
+      x.push_back(d);
+      y.push_back(col[d]);
+    }
+  }
+  if (x.size() < 2) return fail(H3D_EARG, "fewer than two finite dispersion points");
+  std::vector<double> out;
+  int rc;
+  if (weighted)
+    rc = h3dhost::weighted_lowess_fit_eval(x, y, y[0], frac, auto_frac_factor, xs, &out);
+  else
+    rc = h3dhost::lowess_fit_eval(x, y, y[0], frac >= 0 ? frac : 0.3, 0.01, xs, &out);
+  if (rc) return fail(H3D_ENOCONV, "lowess fit failed (degenerate dispersion table)");
+  std::memcpy(table_out, out.data(), D * 8);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// lrt
+// ---------------------------------------------------------------------------
+
+int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                const int32_t* d_dist, const double* disp_table, int64_t n,
+                int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
+                double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
+                double* d_disp) {
+  if (!ctx || !disp_table || !cond_of_rep) return fail(H3D_EARG, "null argument");
+  if (n == 0) return 0;
+  if (!d_raw || !d_f || !d_p || !d_llr || !d_mu0 || !d_mu1)
+    return fail(H3D_EARG, "null device buffer");
+  std::vector<int> nrep;
+  std::vector<int32_t> rep_idx;
+  if (int rc = check_cond(cond_of_rep, R, C, &nrep, &rep_idx)) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  // d_dist == NULL: disp_table holds per-pixel dispersions (n, C)
+  const size_t tab_n = d_dist ? (size_t)D * C : (size_t)n * C;
+  double* d_tab = (double*)scratch(ctx, "disp_table", tab_n * 8);
+  int32_t* d_cond = (int32_t*)scratch(ctx, "cond_of_rep", R * 4);
+  int* d_fl = (int*)scratch(ctx, "lrt_flags", 4);
+  if (!d_tab || !d_cond || !d_fl) return fail(H3D_ENOMEM, "lrt scratch");
+  HIP_TRY(hipMemcpyAsync(d_tab, disp_table, tab_n * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_cond, cond_of_rep, R * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
+  const int grid = grid_for(ctx, n, 16);
+  {
+    ProfScope ps(ctx, "lrt", n);
+    const int m = R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
+    const int cm = C <= 2 ? 2 : C <= 4 ? 4 : 8;
+#define H3D_LRT(MM, CC)                                                          \
+  launch_lrt<MM, CC>(ctx, grid, d_raw, d_f, d_dist, d_tab, n, R, C, D, d_cond,   \
+                     refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, d_fl)
+    if (m == 4 && cm == 2) H3D_LRT(4, 2);
+    else if (m == 4 && cm == 4) H3D_LRT(4, 4);
+    else if (m == 8 && cm == 2) H3D_LRT(8, 2);
+    else if (m == 8 && cm == 4) H3D_LRT(8, 4);
+    else if (m == 16 && cm == 2) H3D_LRT(16, 2);
+    else if (m == 16 && cm == 4) H3D_LRT(16, 4);
+    else if (m <= 16) H3D_LRT(16, 8);
+    else H3D_LRT(32, 8);
+#undef H3D_LRT
+  }
+  HIP_TRY(hipGetLastError());
+  int fl = 0;
+  HIP_TRY(hipMemcpyAsync(&fl, d_fl, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return flags_to_code(fl);
+}
+
+int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
+            const int32_t* dist, const double* disp_table, int64_t n, int R,
+            int C, const int32_t* cond_of_rep, int D, int refit_mu, double* p,
+            double* llr, double* mu0, double* mu1, double* disp_out) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  if (n == 0) return 0;
+  if (!raw || !f || !p || !llr || !mu0 || !mu1) return fail(H3D_EARG, "null buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  int64_t* d_raw64 = (int64_t*)scratch(ctx, "in_raw64", n * R * 8);
+  int32_t* d_raw = (int32_t*)scratch(ctx, "in_raw", n * R * 4);
+  double* d_f = (double*)scratch(ctx, "in_f", n * R * 8);
+  int32_t* d_dist = dist ? (int32_t*)scratch(ctx, "in_dist", n * 4) : nullptr;
+  double* d_out = (double*)scratch(ctx, "lrt_out", n * (3 + 2 * C) * 8);
+  int* d_ovf = (int*)scratch(ctx, "ovf", 4);
+  if (!d_raw64 || !d_raw || !d_f || (dist && !d_dist) || !d_out || !d_ovf)
+    return fail(H3D_ENOMEM, "lrt inputs");
+  HIP_TRY(hipMemcpyAsync(d_raw64, raw, n * R * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_f, f, n * R * 8, hipMemcpyHostToDevice, s));
+  if (dist) HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(d_ovf, 0, 4, s));
+  hipLaunchKernelGGL(k_i64_to_i32, dim3(grid_for(ctx, n * R)), dim3(kBlock), 0, s,
+                     d_raw64, d_raw, n * R, d_ovf);
+  double *dp = d_out, *dl = d_out + n, *dm0 = d_out + 2 * n, *dm1 = d_out + 3 * n,
+         *dd = d_out + (3 + C) * n;
+  int rc = h3d_lrt_dev(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep,
+                       D, refit_mu, dp, dl, dm0, dm1, disp_out ? dd : nullptr);
+  int ovf = 0;
+  HIP_TRY(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(p, dp, n * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(llr, dl, n * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(mu0, dm0, n * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(mu1, dm1, n * C * 8, hipMemcpyDeviceToHost, s));
+  if (disp_out) HIP_TRY(hipMemcpyAsync(disp_out, dd, n * C * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (ovf) return fail(H3D_EINPUT, "raw counts must be in [0, 2^31)");
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// bh
+// ---------------------------------------------------------------------------
+
+int h3d_bh(const double* p, int64_t n, double* q) {
+  if (n < 0 || (n > 0 && (!p || !q))) return fail(H3D_EARG, "null argument");
+  h3dhost::bh(p, n, q);
+  return 0;
+}
+
+}  // extern "C"
+
+#include "h3d_prepare_api.h"

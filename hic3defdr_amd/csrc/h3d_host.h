@@ -1,0 +1,378 @@
+// Host-side numerics of the hot path that act on per-distance tables
+// (<= dist_thresh_max + 1 points): the dispersion-vs-distance smoother and
+// BH. They run once per condition on a few hundred values, so they stay on
+// the host CPU inside libh3d.so; everything per-pixel runs on the GPU.
+//
+// Restated algorithms (op-for-op, so the tables match the reference's bits):
+//   * pandas 2.x rolling(window, center=True).var() (Welford + Kahan, the
+//     consecutive-equal-values rule) -> reference lowess.py:173
+//   * statsmodels 0.12 lowess (tricube / bisquare, delta skipping, ties)
+//     -> lib5c lowess, reference lowess.py:72
+//   * numpy pairwise summation where the reference sums with numpy
+//   * scipy interp1d linear with extrapolation
+//   * weighted_lowess_fit / lowess_fit -> reference lowess.py:10-244
+//   * BH = statsmodels fdrcorrection (lib5c adjust_pvalues, analysis.py:300)
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <numeric>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace h3dhost {
+
+// numpy pairwise_sum (PW_BLOCKSIZE 128)
+inline double np_pairwise(const double* a, int64_t n) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int64_t i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+// pandas Series.rolling(window=w, center=True).var() (ddof=1, min_periods=w)
+inline std::vector<double> rolling_var_center(const std::vector<double>& v,
+                                              int w) {
+  const int64_t n = (int64_t)v.size();
+  std::vector<double> out(n, NAN);
+  const int64_t offset = (w - 1) / 2;
+  std::vector<int64_t> st(n), en(n);
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t e = i + 1 + offset, s = e - w;
+    en[i] = std::min<int64_t>(std::max<int64_t>(e, 0), n);
+    st[i] = std::min<int64_t>(std::max<int64_t>(s, 0), n);
+  }
+  double mean_x = 0, ssqdm = 0, nobs = 0, comp_add = 0, comp_rem = 0, prev = 0;
+  int64_t consec = 0;
+  auto add = [&](double val) {
+    if (val != val) return;
+    nobs += 1;
+    if (val == prev)
+      consec += 1;
+    else
+      consec = 1;
+    prev = val;
+    double prev_mean = mean_x - comp_add;
+    double y = val - comp_add;
+    double t = y - mean_x;
+    comp_add = t + mean_x - y;
+    double delta = t;
+    if (nobs)
+      mean_x = mean_x + delta / nobs;
+    else
+      mean_x = 0;
+    ssqdm = ssqdm + (val - prev_mean) * (val - mean_x);
+  };
+  auto rem = [&](double val) {
+    if (val == val) {
+      nobs -= 1;
+      if (nobs) {
+        double prev_mean = mean_x - comp_rem;
+        double y = val - comp_rem;
+        double t = y - mean_x;
+        comp_rem = t + mean_x - y;
+        double delta = t;
+        mean_x = mean_x - delta / nobs;
+        ssqdm = ssqdm - (val - prev_mean) * (val - mean_x);
+      } else {
+        mean_x = 0;
+        ssqdm = 0;
+      }
+    }
+  };
+  const int64_t minp = std::max<int64_t>(w, 1);
+  for (int64_t i = 0; i < n; ++i) {
+    if (i == 0 || st[i] >= en[i - 1]) {
+      prev = v[st[i]];
+      consec = 0;
+      mean_x = ssqdm = nobs = comp_add = comp_rem = 0;
+      for (int64_t j = st[i]; j < en[i]; ++j) add(v[j]);
+    } else {
+      for (int64_t j = st[i - 1]; j < st[i]; ++j) rem(v[j]);
+      for (int64_t j = en[i - 1]; j < en[i]; ++j) add(v[j]);
+    }
+    if (nobs >= minp && nobs > 1) {
+      out[i] = (nobs == 1 || consec >= nobs) ? 0.0 : ssqdm / (nobs - 1.0);
+    } else {
+      out[i] = NAN;
+    }
+  }
+  return out;
+}
+
+// statsmodels lowess on x sorted ascending (it robustness iterations)
+inline std::vector<double> lowess_sorted(const std::vector<double>& x,
+                                         const std::vector<double>& y,
+                                         double frac, int it, double delta) {
+  const int64_t n = (int64_t)x.size();
+  int64_t k = (int64_t)(frac * n + 1e-10);
+  k = std::min<int64_t>(std::max<int64_t>(k, 2), n);
+  std::vector<double> resid_w(n, 1.0), y_fit(n, 0.0), w(n);
+  for (int rob = 0; rob <= it; ++rob) {
+    std::fill(y_fit.begin(), y_fit.end(), 0.0);
+    int64_t i = 0, last_fit_i = -1, left = 0, right = k;
+    while (true) {
+      const double xval = x[i];
+      while (right < n && xval > (x[left] + x[right]) / 2.0) {
+        ++left;
+        ++right;
+      }
+      const double radius = std::fmax(xval - x[left], x[right - 1] - xval);
+      const int64_t m = right - left;
+      for (int64_t j = 0; j < m; ++j) {
+        double t = std::fabs(x[left + j] - xval) / radius;
+        double c = t * (t * t);
+        double u = 1 - c;
+        u = u > 0.0 ? u : 0.0;
+        double wt = u * (u * u);
+        if (rob > 0) wt = wt * resid_w[left + j];
+        w[j] = wt;
+      }
+      const double sw = np_pairwise(w.data(), m);
+      if (sw <= 0.0) {
+        y_fit[i] = y[i];
+      } else {
+        for (int64_t j = 0; j < m; ++j) w[j] = w[j] / sw;
+        double swx = 0.0;
+        for (int64_t j = 0; j < m; ++j) swx += w[j] * x[left + j];
+        double sq = 0.0;
+        for (int64_t j = 0; j < m; ++j) {
+          double dv = x[left + j] - swx;
+          sq += w[j] * (dv * dv);
+        }
+        double acc = 0.0;
+        for (int64_t j = 0; j < m; ++j) {
+          double p = w[j] * (1.0 + (xval - swx) * (x[left + j] - swx) / sq);
+          acc += p * y[left + j];
+        }
+        y_fit[i] = acc;
+      }
+      if (last_fit_i < i - 1) {
+        const double den = x[i] - x[last_fit_i];
+        for (int64_t j = last_fit_i + 1; j < i; ++j) {
+          double a = (x[j] - x[last_fit_i]) / den;
+          y_fit[j] = a * y_fit[i] + (1.0 - a) * y_fit[last_fit_i];
+        }
+      }
+      last_fit_i = i;
+      const double cut = x[i] + delta;
+      int64_t kk = last_fit_i;
+      for (int64_t q = last_fit_i + 1; q < n; ++q) {
+        kk = q;
+        if (x[q] > cut) break;
+        if (x[q] == x[last_fit_i]) {
+          y_fit[q] = y_fit[last_fit_i];
+          last_fit_i = q;
+        }
+      }
+      i = std::max(kk - 1, last_fit_i + 1);
+      if (last_fit_i >= n - 1) break;
+    }
+    if (rob < it) {
+      std::vector<double> ab(n), res(n);
+      for (int64_t j = 0; j < n; ++j) {
+        res[j] = y[j] - y_fit[j];
+        ab[j] = std::fabs(res[j]);
+      }
+      std::vector<double> srt(ab);
+      std::sort(srt.begin(), srt.end());
+      const double med = (n % 2) ? srt[n / 2]
+                                 : 0.5 * (srt[n / 2 - 1] + srt[n / 2]);
+      const double s6 = 6.0 * med;
+      for (int64_t j = 0; j < n; ++j) {
+        if (s6 > 0) {
+          double t = std::fabs(res[j] / s6);
+          resid_w[j] = (t < 1.0) ? (1 - t * t) * (1 - t * t) : 0.0;
+        } else {
+          resid_w[j] = (res[j] == 0) ? 1.0 : 0.0;
+        }
+      }
+    }
+  }
+  return y_fit;
+}
+
+// scipy interp1d(kind='linear', fill_value='extrapolate') at one point
+inline double interp_extrap(const std::vector<double>& xp,
+                            const std::vector<double>& yp, double xn) {
+  const int64_t m = (int64_t)xp.size();
+  int64_t idx = std::lower_bound(xp.begin(), xp.end(), xn) - xp.begin();
+  idx = std::min<int64_t>(std::max<int64_t>(idx, 1), m - 1);
+  const int64_t lo = idx - 1, hi = idx;
+  const double slope = (yp[hi] - yp[lo]) / (xp[hi] - xp[lo]);
+  return slope * (xn - xp[lo]) + yp[lo];
+}
+
+// lowess_fit (lowess.py:10-92, logx=logy=False) evaluated at xs
+inline int lowess_fit_eval(const std::vector<double>& x,
+                           const std::vector<double>& y, double left_boundary,
+                           double frac, double delta_frac,
+                           const std::vector<double>& xs,
+                           std::vector<double>* out) {
+  const int64_t n = (int64_t)x.size();
+  if (n < 2) return -1;
+  std::vector<int64_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int64_t a, int64_t b) { return x[a] < x[b]; });
+  std::vector<double> sx(n), sy(n);
+  for (int64_t i = 0; i < n; ++i) {
+    sx[i] = x[order[i]];
+    sy[i] = y[order[i]];
+  }
+  const double delta = (sx[n - 1] - sx[0]) * delta_frac;
+  std::vector<double> fit = lowess_sorted(sx, sy, frac, 3, delta);
+  std::vector<double> ux, uy;  // np.unique(sorted_x, return_index=True)
+  for (int64_t i = 0; i < n; ++i)
+    if (i == 0 || sx[i] != sx[i - 1]) {
+      ux.push_back(sx[i]);
+      uy.push_back(fit[i]);
+    }
+  if (ux.size() < 2) return -1;
+  out->resize(xs.size());
+  for (size_t j = 0; j < xs.size(); ++j) {
+    double v = interp_extrap(ux, uy, xs[j]);
+    if (xs[j] <= left_boundary) v = fit[0];
+    (*out)[j] = v;
+  }
+  return 0;
+}
+
+// weighted_lowess_fit (lowess.py:95-244) evaluated at xs
+inline int weighted_lowess_fit_eval(std::vector<double> x, std::vector<double> y,
+                                    double left_boundary, double frac,
+                                    double auto_frac_factor,
+                                    const std::vector<double>& xs,
+                                    std::vector<double>* out) {
+  const int64_t n = (int64_t)y.size();
+  if (n < 2) return -1;
+  {
+    std::vector<int64_t> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t a, int64_t b) { return x[a] < x[b]; });
+    std::vector<double> sx(n), sy(n);
+    for (int64_t i = 0; i < n; ++i) {
+      sx[i] = x[order[i]];
+      sy[i] = y[order[i]];
+    }
+    x.swap(sx);
+    y.swap(sy);
+  }
+  std::vector<double> var = rolling_var_center(y, 20);
+  std::vector<double> weight(n, NAN);
+  for (int64_t i = 0; i < n; ++i) {
+    double prec = 1.0 / var[i];
+    if (std::isfinite(prec)) weight[i] = std::pow(prec, 0.25);
+  }
+  double min_w = INFINITY;
+  bool any = false;
+  for (double v : weight)
+    if (v == v) {
+      min_w = std::min(min_w, v);
+      any = true;
+    }
+  if (!any) return -1;  // np.nanmin of all-NaN raises in the reference
+  std::vector<double> sw(n);
+  const double inv = 1.0 / min_w;
+  for (int64_t i = 0; i < n; ++i) sw[i] = weight[i] * inv;
+  // Pinned deviation: the reference scales so that the smallest
+  // weight is 1 (lowess.py:183-184), but w * (1 / w) rounds to 1 - 2^-53 for
+  // ~13% of doubles, and floor() then drops that point from the fit. Whether
+  // it happens depends on the last bit of w, i.e. on ulp-level details of
+  // the per-distance dispersions that no reimplementation reproduces; the
+  // intended value 1 is used instead.
+  for (int64_t i = 0; i < n; ++i)
+    if (weight[i] == min_w) sw[i] = 1.0;
+  double max_w = -INFINITY;
+  for (double v : sw)
+    if (v == v) max_w = std::max(max_w, v);
+  for (auto& v : sw)
+    if (std::isinf(v)) v = max_w;
+  int64_t first_finite = 0;
+  while (first_finite < n && !std::isfinite(sw[first_finite])) ++first_finite;
+  const double left_w = sw[first_finite < n ? first_finite : 0];
+  for (int64_t i = 0; i < n; ++i) {
+    if (sw[i] != sw[i]) {
+      if ((double)i < n / 2.0)
+        sw[i] = left_w;
+      else if ((double)i > n / 2.0)
+        sw[i] = 1;
+    }
+    if (!std::isfinite(sw[i])) return -1;  // reference assert
+  }
+  int64_t inc_idx = 0;
+  for (int64_t i = 0; i + 1 < n; ++i)
+    if (y[i + 1] - y[i] > 0) {
+      inc_idx = i;
+      break;
+    }
+  inc_idx += 1;
+  std::vector<double> ex, ey;
+  for (int64_t i = inc_idx; i < n; ++i) {
+    int64_t m = (int64_t)std::floor(sw[i]);
+    for (int64_t j = 0; j < m; ++j) {
+      ex.push_back(x[i]);
+      ey.push_back(y[i]);
+    }
+  }
+  if (!(frac >= 0)) {
+    std::vector<double> fw;
+    for (double v : weight)
+      if (v == v) fw.push_back(v);
+    const double nanmean = np_pairwise(fw.data(), (int64_t)fw.size()) /
+                           (double)fw.size();
+    const double frac_auto = auto_frac_factor / (max_w * nanmean);
+    frac = std::max(std::min(frac_auto, 2. / 3), 0.05);
+  }
+  std::vector<double> fit;
+  if (lowess_fit_eval(ex, ey, left_boundary, frac, 0.01, xs, &fit)) return -1;
+  out->resize(xs.size());
+  for (size_t j = 0; j < xs.size(); ++j) {
+    double v = fit[j];
+    if (xs[j] < x[inc_idx]) {
+      v = interp_extrap(x, y, xs[j]);
+      if (xs[j] < x[0]) v = y[0];
+    }
+    (*out)[j] = v;
+  }
+  return 0;
+}
+
+// BH over finite p-values (statsmodels fdrcorrection, indep), NaN elsewhere
+inline void bh(const double* p, int64_t n, double* q) {
+  std::vector<int64_t> idx;
+  idx.reserve(n);
+  for (int64_t i = 0; i < n; ++i) {
+    if (std::isfinite(p[i]))
+      idx.push_back(i);
+    else
+      q[i] = NAN;
+  }
+  const int64_t m = (int64_t)idx.size();
+  std::stable_sort(idx.begin(), idx.end(),
+                   [&](int64_t a, int64_t b) { return p[a] < p[b]; });
+  std::vector<double> qs(m);
+  for (int64_t j = 0; j < m; ++j)
+    qs[j] = p[idx[j]] / ((double)(j + 1) / (double)m);
+  for (int64_t j = m - 2; j >= 0; --j) qs[j] = std::min(qs[j], qs[j + 1]);
+  for (int64_t j = 0; j < m; ++j) q[idx[j]] = qs[j] > 1 ? 1.0 : qs[j];
+}
+
+}  // namespace h3dhost

@@ -5,9 +5,14 @@
 // against scipy / the oracle without a GPU. The product never loads this
 // library (hic3defdr_amd loads libh3d.so and fails loudly without it).
 #include <cstdint>
+#include <vector>
 
 #include "h3d_model.h"
 #include "h3d_special.h"
+
+namespace {
+constexpr int M = h3d::kMaxReps;
+}
 
 extern "C" {
 
@@ -15,10 +20,10 @@ extern "C" {
   void h3dt_##name(int64_t n, const double* x, double* out) { \
     for (int64_t i = 0; i < n; ++i) out[i] = h3d::fn(x[i]);   \
   }
-#define H3DT_BINARY(name, fn)                                              \
-  void h3dt_##name(int64_t n, const double* a, const double* x,           \
-                   double* out) {                                          \
-    for (int64_t i = 0; i < n; ++i) out[i] = h3d::fn(a[i], x[i]);         \
+#define H3DT_BINARY(name, fn)                                     \
+  void h3dt_##name(int64_t n, const double* a, const double* x,  \
+                   double* out) {                                 \
+    for (int64_t i = 0; i < n; ++i) out[i] = h3d::fn(a[i], x[i]); \
   }
 
 H3DT_UNARY(lgam, lgam)
@@ -37,20 +42,20 @@ int h3dt_fit_mu(int64_t n, int r, const int32_t* x, const double* b,
                 const double* alpha, double* mu) {
   int bad = 0;
   for (int64_t i = 0; i < n; ++i) {
-    double xs[h3d::kMaxReps], bs[h3d::kMaxReps], as[h3d::kMaxReps];
+    double xs[M], bs[M], as[M];
     for (int k = 0; k < r; ++k) {
       xs[k] = x[i * r + k];
       bs[k] = b[i * r + k];
       as[k] = alpha[i * r + k];
     }
     int st = 0;
-    mu[i] = h3d::fit_mu(xs, bs, as, r, &st);
+    mu[i] = h3d::fit_mu<M>(xs, bs, as, r, ~0u, &st);
     bad |= st;
   }
   return bad;
 }
 
-// q2qnbinom elementwise (no in-place clamp carry; single replicate)
+// q2qnbinom elementwise (single replicate, no clamp carry)
 void h3dt_q2q(int64_t n, const double* x, const double* mu_in,
               const double* mu_out, const double* alpha, double* out) {
   for (int64_t i = 0; i < n; ++i) {
@@ -64,12 +69,12 @@ int h3dt_equalize(int64_t n, int r, const int32_t* x, const double* f,
                   double alpha, double* out) {
   int bad = 0;
   for (int64_t i = 0; i < n; ++i) {
-    double xs[h3d::kMaxReps], fs[h3d::kMaxReps], ps[h3d::kMaxReps];
+    double xs[M], fs[M], ps[M];
     for (int k = 0; k < r; ++k) {
       xs[k] = x[i * r + k];
       fs[k] = f[i * r + k];
     }
-    bad |= h3d::equalize_pixel(xs, fs, r, alpha, ps);
+    bad |= h3d::equalize_pixel<M>(xs, fs, r, alpha, ps);
     for (int k = 0; k < r; ++k) out[i * r + k] = ps[k];
   }
   return bad;
@@ -80,53 +85,47 @@ int h3dt_lrt(int64_t n, int R, int C, const int32_t* raw, const double* f,
              const double* disp_wide, const int32_t* cond_of_rep, int refit,
              double* p, double* llr, double* mu0, double* mu1) {
   int bad = 0;
+  int cond[M];
+  for (int k = 0; k < R; ++k) cond[k] = cond_of_rep[k];
   for (int64_t i = 0; i < n; ++i) {
-    double xs[h3d::kMaxReps], fs[h3d::kMaxReps], as[h3d::kMaxReps];
+    double xs[M], fs[M], as[M];
     for (int k = 0; k < R; ++k) {
       xs[k] = raw[i * R + k];
       fs[k] = f[i * R + k];
       as[k] = disp_wide[i * R + k];
     }
     double m1[h3d::kMaxConds];
-    bad |= h3d::lrt_pixel(xs, fs, as, cond_of_rep, R, C, refit != 0, &p[i],
-                          &llr[i], &mu0[i], m1);
+    bad |= h3d::lrt_pixel<M, h3d::kMaxConds>(xs, fs, as, cond, R, C,
+                                             refit != 0, &p[i], &llr[i],
+                                             &mu0[i], m1);
     for (int c = 0; c < C; ++c) mu1[i * C + c] = m1[c];
   }
   return bad;
 }
 
-// cml NLL per-pixel term (dispersion.py:67-70) summed over a segment
-double h3dt_nll(int64_t n, int r, const double* data, double delta) {
-  double s = 0.0;
-  h3d::NllConst k = h3d::nll_const(delta, r);
-  for (int64_t i = 0; i < n; ++i) s += h3d::nll_pixel(data + i * r, r, k);
-  return -s;
-}
-
-// full qcml on one segment with the shared Brent state machine
+// full qcml on one segment, driven by the same state machine as the kernels
 double h3dt_qcml(int64_t n, int r, const int32_t* x, const double* f,
                  int* status) {
-  double* pseudo = new double[n * r];
+  std::vector<double> pseudo(n * r);
   h3d::SegState st;
-  h3d::seg_init(&st, n);
+  h3d::seg_init(&st, n, r);
   int guard = 0;
   while (st.phase != h3d::kDone && guard++ < 100000) {
     double total = 0.0;
     if (st.phase == h3d::kEqualize) {
       for (int64_t i = 0; i < n; ++i) {
-        double xs[h3d::kMaxReps], fs[h3d::kMaxReps];
+        double xs[M], fs[M];
         for (int k = 0; k < r; ++k) {
           xs[k] = x[i * r + k];
           fs[k] = f[i * r + k];
         }
-        st.flags |= h3d::equalize_pixel(xs, fs, r, st.disp, pseudo + i * r);
+        st.flags |= h3d::equalize_pixel<M>(xs, fs, r, st.disp, &pseudo[i * r]);
       }
     }
-    h3d::NllConst kc = h3d::nll_const(st.x, r);
-    for (int64_t i = 0; i < n; ++i) total += h3d::nll_pixel(pseudo + i * r, r, kc);
-    h3d::seg_step(&st, total);
+    for (int64_t i = 0; i < n; ++i)
+      total += h3d::nll_pixel<M>(&pseudo[i * r], r, st.k);
+    h3d::seg_step(&st, total, r);
   }
-  delete[] pseudo;
   *status = st.flags;
   return st.result;
 }

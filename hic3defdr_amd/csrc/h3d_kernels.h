@@ -1,0 +1,283 @@
+// gfx950 kernels of the hic3defdr hot path (estimate_disp + lrt).
+//
+// Layout in HBM:
+//   * LRT inputs stay in the reference's pixel order, replicate-minor (AoS):
+//     raw (n, R) int32, f (n, R) f64, dist (n) int32 -> one lane per pixel
+//     reads its R contiguous values (16 B / 32 B vector loads for R = 4).
+//   * estimate_disp re-orders the disp pixels by distance once (stable radix
+//     sort on dist) into replicate-major (SoA) copies raw_s[r][i], f_s[r][i]
+//     and the pseudodata buffer pd[r][i], so a segment (distance d) is a
+//     contiguous index range and every per-replicate access is coalesced.
+//   * work items = (chunk of 256 pixels of one distance) x condition; one
+//     256-thread workgroup per work item, one pixel per lane.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "h3d_model.h"
+
+namespace h3d {
+
+constexpr int kChunk = 256;  // pixels per disp work item (= block size)
+constexpr int kBlock = 256;
+
+// deterministic block sum of one double per thread (fixed butterfly per wave,
+// then waves in order); result valid in thread 0.
+__device__ inline double block_sum(double v, double* lds) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) t += lds[w];
+  }
+  return t;
+}
+
+__global__ void k_i64_to_i32(const int64_t* __restrict__ in,
+                             int32_t* __restrict__ out, int64_t n,
+                             int* __restrict__ overflow) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = in[i];
+    if (v < 0 || v > 0x7fffffffLL) atomicOr(overflow, 1);
+    out[i] = (int32_t)v;
+  }
+}
+
+__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int32_t)i;
+}
+
+// AoS (n, R) -> distance-sorted SoA [r][i]
+__global__ void k_gather_soa(const int32_t* __restrict__ perm,
+                             const int32_t* __restrict__ raw,
+                             const double* __restrict__ f, int64_t n, int R,
+                             int32_t* __restrict__ raw_s,
+                             double* __restrict__ f_s) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t src = perm[i];
+    for (int r = 0; r < R; ++r) {
+      raw_s[(int64_t)r * n + i] = raw[src * R + r];
+      f_s[(int64_t)r * n + i] = f[src * R + r];
+    }
+  }
+}
+
+// seg_start[d] = first index with dist_s >= d (d = 0..D)
+__global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
+                             int D, int64_t* __restrict__ seg_start) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > D) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (dist_s[mid] < d)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  seg_start[d] = lo;
+}
+
+// Work item w of the active list: item = chunk * C + c.
+// Equalize pass: per pixel equalize (scaled_nb.py:186-214) with the
+// segment's current dispersion, write pseudodata, then the NLL term at the
+// first Brent point. NLL pass: the NLL term (dispersion.py:67-70) at the
+// segment's current Brent point. Block partial -> partial[w].
+template <int M>
+__global__ __launch_bounds__(kBlock) void k_disp_work(
+    const int32_t* __restrict__ raw_s, const double* __restrict__ f_s,
+    double* __restrict__ pd, int64_t n, const int64_t* __restrict__ chunk_start,
+    const int32_t* __restrict__ chunk_len, const int32_t* __restrict__ chunk_d,
+    int C, const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
+    const int32_t* __restrict__ n_rep /* C */, const SegState* __restrict__ st,
+    int* __restrict__ seg_flags, const int32_t* __restrict__ list,
+    const int32_t* __restrict__ list_len, double* __restrict__ partial) {
+  __shared__ double lds[kBlock / 64];
+  const int len = *list_len;
+  for (int w = blockIdx.x; w < len; w += gridDim.x) {
+    const int item = list[w];
+    const int chunk = item / C, c = item - chunk * C;
+    const int s = chunk_d[chunk] * C + c;
+    const int phase = st[s].phase;
+    const int nr = n_rep[c];
+    double term = 0.0;
+    const int i = threadIdx.x;
+    if (i < chunk_len[chunk]) {
+      const int64_t px = chunk_start[chunk] + i;
+      double d[M];
+      int ri[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) ri[k] = (k < nr) ? rep_idx[c * kMaxReps + k] : 0;
+      if (phase == kEqualize) {
+        double x[M], f[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          if (k < nr) {
+            x[k] = (double)raw_s[(int64_t)ri[k] * n + px];
+            f[k] = f_s[(int64_t)ri[k] * n + px];
+          } else {
+            x[k] = 0.0;
+            f[k] = 1.0;
+          }
+        }
+        const int fl = equalize_pixel<M>(x, f, nr, st[s].disp, d);
+        if (fl) atomicOr(&seg_flags[s], fl);
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+          if (k < nr) pd[(int64_t)ri[k] * n + px] = d[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+          d[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
+      }
+      const NllConst kc = st[s].k;
+      term = nll_pixel<M>(d, nr, kc);
+    }
+    const double t = block_sum(term, lds);
+    if (threadIdx.x == 0) partial[w] = t;
+    __syncthreads();
+  }
+}
+
+// seg_total[s] = sum of the segment's partials in list order (one wave per
+// segment, fixed reduction tree -> deterministic)
+__global__ void k_seg_reduce(const double* __restrict__ partial,
+                             const int32_t* __restrict__ seg_lb,
+                             const int32_t* __restrict__ seg_le, int S,
+                             double* __restrict__ seg_total) {
+  const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= S) return;
+  const int b = seg_lb[s], e = seg_le[s];
+  double v = 0.0;
+  for (int j = b + lane; j < e; j += 64) v += partial[j];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) seg_total[s] = v;
+}
+
+// One workgroup: advance every active segment's qcml/Brent state machine with
+// its (possibly rank-reduced) total, then rebuild the active work list.
+__global__ __launch_bounds__(1024) void k_seg_update(
+    SegState* __restrict__ st, const double* __restrict__ seg_total,
+    const int* __restrict__ seg_flags, int S, int C,
+    const int32_t* __restrict__ n_rep, const int32_t* __restrict__ seg_chunk_b,
+    const int32_t* __restrict__ seg_chunk_e, int32_t* __restrict__ list,
+    int32_t* __restrict__ list_len, int32_t* __restrict__ seg_lb,
+    int32_t* __restrict__ seg_le, double* __restrict__ result,
+    int32_t* __restrict__ active, int first) {
+  __shared__ int32_t scan[1024];
+  __shared__ int32_t base_s;
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  for (int s0 = 0; s0 < S; s0 += blockDim.x) {
+    const int s = s0 + threadIdx.x;
+    int cnt = 0;
+    if (s < S) {
+      SegState cur = st[s];
+      const int c = s % C;
+      if (!first && cur.phase != kDone) {
+        cur.flags |= seg_flags[s];
+        seg_step(&cur, seg_total[s], n_rep[c]);
+        st[s] = cur;
+      }
+      if (cur.phase == kDone) {
+        result[s] = cur.result;
+      } else {
+        cnt = seg_chunk_e[s / C] - seg_chunk_b[s / C];
+      }
+    }
+    scan[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // inclusive scan
+      const int v = (threadIdx.x >= (unsigned)off) ? scan[threadIdx.x - off] : 0;
+      __syncthreads();
+      scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    const int base = base_s;
+    const int beg = base + scan[threadIdx.x] - cnt;
+    if (s < S) {
+      seg_lb[s] = beg;
+      seg_le[s] = beg + cnt;
+      const int d = s / C, c = s % C;
+      const int cb = seg_chunk_b[d];
+      for (int j = 0; j < cnt; ++j) list[beg + j] = (cb + j) * C + c;
+    }
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) base_s = base + scan[threadIdx.x];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *list_len = base_s;
+    *active = base_s;
+  }
+}
+
+// Per-pixel LRT (lrt.py:7-50) in the reference pixel order; disp from the
+// (D, C) table (analysis.py:218: disp = disp_fn(dist), evaluated per d).
+template <int M, int CM>
+__global__ __launch_bounds__(kBlock) void k_lrt(
+    const int32_t* __restrict__ raw, const double* __restrict__ f,
+    const int32_t* __restrict__ dist, const double* __restrict__ table,
+    int64_t n, int R, int C, int D, const int32_t* __restrict__ cond_of_rep,
+    int refit, double* __restrict__ p, double* __restrict__ llr,
+    double* __restrict__ mu0, double* __restrict__ mu1,
+    double* __restrict__ disp_out, int* __restrict__ flags) {
+  int cond[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) cond[k] = (k < R) ? cond_of_rep[k] : -1;
+  int fl_all = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    // dist == nullptr: `table` holds per-pixel dispersions (n, C)
+    const int d = dist ? dist[i] : 0;
+    const double* trow = dist ? table + (int64_t)d * C : table + i * C;
+    const bool inb = dist ? (d >= 0 && d < D) : true;
+    double dc[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) dc[c] = (c < C && inb) ? trow[c] : NAN;
+    double x[M], fv[M], a[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      if (k < R) {
+        x[k] = (double)raw[i * R + k];
+        fv[k] = f[i * R + k];
+        double ak = 0.0;
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c == cond[k]) ak = dc[c];
+        a[k] = ak;
+      } else {
+        x[k] = 0.0;
+        fv[k] = 1.0;
+        a[k] = 1.0;
+      }
+    }
+    double pv, lv, m0, m1[CM];
+    fl_all |= lrt_pixel<M, CM>(x, fv, a, cond, R, C, refit != 0, &pv, &lv, &m0,
+                               m1);
+    p[i] = pv;
+    llr[i] = lv;
+    mu0[i] = m0;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        mu1[i * C + c] = m1[c];
+        if (disp_out) disp_out[i * C + c] = dc[c];
+      }
+  }
+  if (fl_all) atomicOr(flags, fl_all);
+}
+
+}  // namespace h3d

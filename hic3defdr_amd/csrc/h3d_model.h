@@ -1,6 +1,12 @@
 // Scaled negative-binomial model pieces shared by the gfx950 kernels and the
 // host unit-test build. Each function cites the reference code it restates
 // (reference = thomasgilgenast/hic3defdr 0.2.1).
+//
+// Register discipline: per-pixel replicate vectors live in fixed-size local
+// arrays of M slots (M a template constant >= the runtime count n), and every
+// loop runs over all M slots with an `k < n` (or mask) predicate. After
+// inlining and unrolling, every array index is a compile-time constant, so
+// the arrays stay in VGPRs on gfx950 instead of spilling to scratch.
 #pragma once
 
 #include <cmath>
@@ -9,8 +15,8 @@
 
 namespace h3d {
 
-constexpr int kMaxReps = 32;   // replicates per pixel (R)
-constexpr int kMaxConds = 8;   // conditions (C)
+constexpr int kMaxReps = 32;  // replicates per pixel (R)
+constexpr int kMaxConds = 8;  // conditions (C)
 
 // status flags (OR-ed per pixel / per segment, reported by the C ABI)
 constexpr int kFlagNoRoot = 1;     // all-zero counts: no MLE (ref: ValueError)
@@ -19,66 +25,78 @@ constexpr int kFlagBrentFail = 4;  // bounded Brent not successful (ref: assert)
 constexpr int kFlagQcmlGuard = 8;  // qcml exceeded 1000 iterations
 constexpr int kFlagBadInput = 16;  // alpha/b not positive finite (ref: assert)
 
-// numpy's row-sum association for short contiguous rows (pairwise_sum with
-// n <= 128: sequential below 8, eight accumulators from 8 on).
+// numpy's row-sum association for a short contiguous row of n <= M values
+// (pairwise_sum with n <= 128: sequential below 8, eight accumulators from 8).
+template <int M>
 H3D_HD double np_sum(const double* v, int n) {
   if (n < 8) {
     double res = 0.0;
-    for (int i = 0; i < n; ++i) res += v[i];
+#pragma unroll
+    for (int i = 0; i < (M < 8 ? M : 8); ++i)
+      if (i < n) res += v[i];
     return res;
   }
-  double r0 = v[0], r1 = v[1], r2 = v[2], r3 = v[3], r4 = v[4], r5 = v[5],
-         r6 = v[6], r7 = v[7];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-    r0 += v[i];
-    r1 += v[i + 1];
-    r2 += v[i + 2];
-    r3 += v[i + 3];
-    r4 += v[i + 4];
-    r5 += v[i + 5];
-    r6 += v[i + 6];
-    r7 += v[i + 7];
+  if constexpr (M >= 8) {
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = v[j];
+    const int blk = n - (n % 8);
+#pragma unroll
+    for (int i = 8; i < M; ++i)
+      if (i < blk) r[i % 8] += v[i];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int i = 8; i < M; ++i)
+      if (i >= blk && i < n) res += v[i];
+    return res;
   }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += v[i];
-  return res;
+  return NAN;
 }
 
 // MLE of mu under fixed per-replicate dispersion: root of
 //   S(mu) = sum_k (x_k - mu b_k) / (mu + a_k mu^2 b_k)      (scaled_nb.py:143-147)
+// over the replicates k < n with bit k of `mask` set.
 // The reference finds it with scipy's array secant + a brentq fallback
 // (scaled_nb.py:149-181). The log-likelihood is strictly concave in
 // theta = log(mu), so the root is unique; here it is found per lane by
 // Newton on g(theta) = mu S(mu) inside a shrinking bracket (bisection
 // safeguard), to full double precision.
-H3D_HD double fit_mu(const double* x, const double* b, const double* a, int r,
-                     int* status) {
+template <int M>
+H3D_HD double fit_mu(const double* x, const double* b, const double* a, int n,
+                     unsigned mask, int* status) {
   double sx = 0.0, init = 0.0;
-  for (int k = 0; k < r; ++k) {
-    if (!(a[k] > 0.0) || !(b[k] > 0.0) || is_inf(a[k]) || is_inf(b[k]) ||
-        !(x[k] >= 0.0)) {
-      *status |= kFlagBadInput;
-      return NAN;
+  int cnt = 0;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+    if (k < n && ((mask >> k) & 1u)) {
+      bad |= !(a[k] > 0.0) || !(b[k] > 0.0) || is_inf(a[k]) || is_inf(b[k]) ||
+             !(x[k] >= 0.0);
+      sx += x[k];
+      init += x[k] / b[k];
+      ++cnt;
     }
-    sx += x[k];
-    init += x[k] / b[k];
+  if (bad) {
+    *status |= kFlagBadInput;
+    return NAN;
   }
   if (!(sx > 0.0)) {
     *status |= kFlagNoRoot;
     return NAN;
   }
-  double th = log(init / r);
+  double th = log(init / cnt);
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
-    double mu = exp(th);
+    const double mu = exp(th);
     double g = 0.0, gp = 0.0;
-    for (int k = 0; k < r; ++k) {
-      double mb = mu * b[k];
-      double den = 1.0 / (1.0 + a[k] * mb);
-      g += (x[k] - mb) * den;
-      gp -= mb * (1.0 + a[k] * x[k]) * den * den;
-    }
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+      if (k < n && ((mask >> k) & 1u)) {
+        const double mb = mu * b[k];
+        const double den = 1.0 / (1.0 + a[k] * mb);
+        g += (x[k] - mb) * den;
+        gp -= mb * (1.0 + a[k] * x[k]) * den * den;
+      }
     if (g > 0.0)
       lo = th;
     else if (g < 0.0)
@@ -94,7 +112,7 @@ H3D_HD double fit_mu(const double* x, const double* b, const double* a, int r,
       else
         tn = 0.5 * (lo + hi);
     }
-    double step = fabs(tn - th);
+    const double step = fabs(tn - th);
     th = tn;
     if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp(th);
     if (!is_inf(lo) && !is_inf(hi) && (hi - lo) <= 4e-16 * fmax(1.0, fabs(th)))
@@ -126,12 +144,12 @@ H3D_HD double norm_ppf(double q, double loc, double scale) {
   return ndtri(q) * scale + loc;
 }
 H3D_HD double gamma_sf(double x, double shape, double scale) {
-  double xs = x / scale;
+  const double xs = x / scale;
   if (xs <= 0.0) return 1.0;
   return igamc(shape, xs);
 }
 H3D_HD double gamma_cdf(double x, double shape, double scale) {
-  double xs = x / scale;
+  const double xs = x / scale;
   if (xs <= 0.0) return 0.0;
   return igam(shape, xs);
 }
@@ -174,71 +192,104 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
   return pc;
 }
 
-// equalize for one pixel (scaled_nb.py:186-214) with a scalar dispersion.
-H3D_HD int equalize_pixel(const double* x, const double* f, int r, double alpha,
+// equalize for one pixel (scaled_nb.py:186-214) with a scalar dispersion;
+// x, f: the condition's n replicates (compacted, in design order).
+template <int M>
+H3D_HD int equalize_pixel(const double* x, const double* f, int n, double alpha,
                           double* out) {
-  double lf[kMaxReps], as[kMaxReps];
-  for (int k = 0; k < r; ++k) {
-    lf[k] = log(f[k]);
+  double lf[M], as[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    lf[k] = (k < n) ? log(f[k]) : 0.0;
     as[k] = alpha;
   }
   // gmean(f, pseudocount=0, axis=1) = exp(nanmean(log f)) - 0
-  const double f_mean = exp(np_sum(lf, r) / r) - 0.0;
+  const double f_mean = exp(np_sum<M>(lf, n) / n) - 0.0;
   int st = 0;
-  const double mu = fit_mu(x, f, as, r, &st);
+  const double mu = fit_mu<M>(x, f, as, n, ~0u, &st);
   double mu_out = mu * f_mean;
-  for (int k = 0; k < r; ++k) {
-    double mu_in = mu * f[k];
-    out[k] = q2q(x[k], &mu_in, &mu_out, alpha);
-  }
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+    if (k < n) {
+      double mu_in = mu * f[k];
+      out[k] = q2q(x[k], &mu_in, &mu_out, alpha);
+    }
   return st;
 }
 
 // NB log pmf, mean/dispersion parameterisation (scaled_nb.py:12-33).
 H3D_HD double logpmf(double k, double m, double phi) {
   const double r = 1.0 / phi;
-  const double lr = log(r + m);
-  return lgam(r + k) - lgam(k + 1) - lgam(r) + r * log(r) - r * lr +
-         k * log(m) - k * lr;
+  return lgam(r + k) - lgam(k + 1) - lgam(r) + r * log(r) - r * log(r + m) +
+         k * log(m) - k * log(r + m);
 }
 
-// Per-pixel LRT (lrt.py:7-50). a[k] = disp_wide[k] = disp[cond(k)].
+// masked mean of n values in order (np.mean of the compacted subset)
+template <int M>
+H3D_HD double np_mean_mask(const double* v, int n, unsigned mask) {
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) cnt += (k < n && ((mask >> k) & 1u)) ? 1 : 0;
+  if (cnt < 8) {
+    double res = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+      if (k < n && ((mask >> k) & 1u)) res += v[k];
+    return res / cnt;
+  }
+  double t[M];  // rare (>= 8 replicates per condition): compact then pairwise
+  int j = 0;
+  for (int k = 0; k < n; ++k)
+    if ((mask >> k) & 1u) t[j++] = v[k];
+  return np_sum<M>(t, cnt) / cnt;
+}
+
+// Per-pixel LRT (lrt.py:7-50). a[k] = disp_wide[k] = disp[cond[k]]; CM is a
+// compile-time bound on the number of conditions C.
+template <int M, int CM>
 H3D_HD int lrt_pixel(const double* x, const double* f, const double* a,
-                     const int* cond_of_rep, int R, int C, bool refit,
-                     double* p, double* llr, double* mu0, double* mu1) {
+                     const int* cond, int R, int C, bool refit, double* p,
+                     double* llr, double* mu0, double* mu1) {
   int st = 0;
   if (refit) {
-    *mu0 = fit_mu(x, f, a, R, &st);
-    for (int c = 0; c < C; ++c) {
-      double xs[kMaxReps], fs[kMaxReps], as[kMaxReps];
-      int n = 0;
-      for (int k = 0; k < R; ++k)
-        if (cond_of_rep[k] == c) {
-          xs[n] = x[k];
-          fs[n] = f[k];
-          as[n] = a[k];
-          ++n;
-        }
-      mu1[c] = fit_mu(xs, fs, as, n, &st);
-    }
+    *mu0 = fit_mu<M>(x, f, a, R, ~0u, &st);
   } else {
-    double q[kMaxReps];
-    for (int k = 0; k < R; ++k) q[k] = x[k] / f[k];
-    *mu0 = np_sum(q, R) / R;
-    for (int c = 0; c < C; ++c) {
-      double qs[kMaxReps];
-      int n = 0;
-      for (int k = 0; k < R; ++k)
-        if (cond_of_rep[k] == c) qs[n++] = q[k];
-      mu1[c] = np_sum(qs, n) / n;
+    double q[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) q[k] = (k < R) ? x[k] / f[k] : 0.0;
+    *mu0 = np_sum<M>(q, R) / R;
+  }
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    if (c >= C) break;
+    unsigned mask = 0u;
+#pragma unroll
+    for (int k = 0; k < M; ++k)
+      if (k < R && cond[k] == c) mask |= (1u << k);
+    if (refit) {
+      mu1[c] = fit_mu<M>(x, f, a, R, mask, &st);
+    } else {
+      double q[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) q[k] = (k < R) ? x[k] / f[k] : 0.0;
+      mu1[c] = np_mean_mask<M>(q, R, mask);
     }
   }
-  double tn[kMaxReps], ta[kMaxReps];
-  for (int k = 0; k < R; ++k) {
-    tn[k] = logpmf(x[k], *mu0 * f[k], a[k]);
-    ta[k] = logpmf(x[k], mu1[cond_of_rep[k]] * f[k], a[k]);
+  double tn[M], ta[M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    if (k < R) {
+      double m1 = 0.0;
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c == cond[k]) m1 = mu1[c];
+      tn[k] = logpmf(x[k], *mu0 * f[k], a[k]);
+      ta[k] = logpmf(x[k], m1 * f[k], a[k]);
+    } else {
+      tn[k] = ta[k] = 0.0;
+    }
   }
-  *llr = np_sum(tn, R) - np_sum(ta, R);
+  *llr = np_sum<M>(tn, R) - np_sum<M>(ta, R);
   *p = chi2_sf((double)(C - 1), -2 * *llr);
   return st;
 }
@@ -258,12 +309,15 @@ H3D_HD NllConst nll_const(double delta, int n) {
   return k;
 }
 
-// one pixel's term; nll(delta) = -sum over pixels.
+// one pixel's term sum_k gammaln(d_k + r) + gammaln(n r) - gammaln(z + n r)
+// - n gammaln(r); nll(delta) = -(sum over pixels).
+template <int M>
 H3D_HD double nll_pixel(const double* d, int n, const NllConst& k) {
-  double lg[kMaxReps];
-  for (int j = 0; j < n; ++j) lg[j] = lgam(d[j] + k.r);
-  const double z = np_sum(d, n);
-  return np_sum(lg, n) + k.lg_nr - lgam(z + k.nr) - k.n_lg_r;
+  double lg[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam(d[j] + k.r) : 0.0;
+  const double z = np_sum<M>(d, n);
+  return np_sum<M>(lg, n) + k.lg_nr - lgam(z + k.nr) - k.n_lg_r;
 }
 
 // ---- qcml + bounded Brent as a resumable state machine --------------------
@@ -292,6 +346,7 @@ struct SegState {
   double disp;    // current qcml dispersion (used by the equalize pass)
   double x;       // delta at which the next NLL is evaluated
   double result;  // final qcml dispersion (NaN for an empty segment)
+  NllConst k;     // nll constants at x for n = replicates of the condition
   double a, b, xf, fx, nfc, fnfc, fulc, ffulc, e, rat, xm, tol1, tol2, fu;
 };
 
@@ -301,20 +356,21 @@ H3D_HD double brent_x0() {
   return kBrentA + brent_golden() * (kBrentB - kBrentA);
 }
 
-H3D_HD void seg_init(SegState* s, long long n_px) {
+H3D_HD void seg_init(SegState* s, long long n_px, int n_reps) {
   s->flags = 0;
   s->num = 0;
   s->qiter = 0;
   s->disp = 0.01;
   s->x = brent_x0();
+  s->k = nll_const(s->x, n_reps);
   s->result = NAN;
   s->phase = (n_px > 0) ? kEqualize : kDone;
 }
 
-H3D_HD double sgn(double v) { return (v > 0) - (v < 0); }
+H3D_HD double sgn(double v) { return (double)((v > 0) - (v < 0)); }
 
 // Advance with the NLL pixel-term total evaluated at s->x.
-H3D_HD void seg_step(SegState* s, double total) {
+H3D_HD void seg_step(SegState* s, double total, int n_reps) {
   const double sqrt_eps = brent_sqrt_eps();
   const double golden_mean = brent_golden();
   const double fval = -total;
@@ -357,7 +413,8 @@ H3D_HD void seg_step(SegState* s, double total) {
         s->ffulc = s->fnfc;
         s->nfc = x;
         s->fnfc = fu;
-      } else if ((fu <= s->ffulc) || (s->fulc == s->xf) || (s->fulc == s->nfc)) {
+      } else if ((fu <= s->ffulc) || (s->fulc == s->xf) ||
+                 (s->fulc == s->nfc)) {
         s->fulc = x;
         s->ffulc = fu;
       }
@@ -389,7 +446,7 @@ H3D_HD void seg_step(SegState* s, double total) {
         s->rat = (p + 0.0) / q;
         x = s->xf + s->rat;
         if (((x - s->a) < s->tol2) || ((s->b - x) < s->tol2)) {
-          double si = sgn(s->xm - s->xf) + ((s->xm - s->xf) == 0);
+          const double si = sgn(s->xm - s->xf) + ((s->xm - s->xf) == 0);
           s->rat = s->tol1 * si;
         }
       } else {
@@ -403,8 +460,9 @@ H3D_HD void seg_step(SegState* s, double total) {
         s->e = s->b - s->xf;
       s->rat = golden_mean * s->e;
     }
-    double si = sgn(s->rat) + (s->rat == 0);
+    const double si = sgn(s->rat) + (s->rat == 0);
     s->x = s->xf + si * fmax(fabs(s->rat), s->tol1);
+    s->k = nll_const(s->x, n_reps);
     s->phase = kNll;
     return;
   }
@@ -415,10 +473,10 @@ H3D_HD void seg_step(SegState* s, double total) {
   const double delta = fabs(s->disp - new_disp);
   s->disp = new_disp;
   s->qiter += 1;
-  if (delta > 1e-4 && !(delta < 1e-4) && s->qiter < 1000 &&
-      !(s->flags & kFlagBrentFail)) {
+  if (delta > 1e-4 && s->qiter < 1000 && !(s->flags & kFlagBrentFail)) {
     s->phase = kEqualize;
     s->x = brent_x0();
+    s->k = nll_const(s->x, n_reps);
   } else {
     if (s->qiter >= 1000 && delta > 1e-4) s->flags |= kFlagQcmlGuard;
     s->phase = kDone;

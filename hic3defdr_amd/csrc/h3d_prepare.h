@@ -1,0 +1,288 @@
+// prepare_data kernels: union pixel table of R replicate CSR band matrices
+// (reference util/matrices.py:92-129 + analysis/analysis.py:91-101) and the
+// distance-conditional median-of-ratios size factors (util/scaling.py:68-127,
+// util/binning.py:4-25).
+//
+// Union: every stored entry of every replicate becomes a 64-bit key
+// row * n_bins + col (or a sentinel when it is outside 0 <= col-row <=
+// dist_max, on a bin with zero bias, or zero); one radix sort of (key, entry)
+// groups a pixel's replicate entries into a run; a run is kept when the sum
+// of its deconvoluted values is finite and > 0 (the reference drops zero sums
+// and filters isfinite/>= mean_thresh*R = 0). Keys sort lexicographically in
+// (row, col): the reference's order (csr sum -> tocoo).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace h3d {
+
+struct PrepUnion {
+  int R = 0, n_bins = 0;
+  int64_t n_entries = 0, n_px = 0;
+  // device
+  int64_t* keys_sorted = nullptr;  // n_entries
+  int32_t* ent_sorted = nullptr;   // n_entries
+  int32_t* run_of = nullptr;       // n_entries (exclusive-scanned heads)
+  int32_t* px_of_run = nullptr;    // runs -> pixel (or -1)
+  int64_t* run_start = nullptr;    // runs + 1
+  double* ent_val = nullptr;       // raw value per entry (summed duplicates not needed: canonical CSR)
+  int32_t* ent_rep = nullptr;      // replicate per entry
+  double* bias = nullptr;          // (n_bins, R)
+  int64_t n_runs = 0;
+};
+
+// row id of every CSR entry (one thread per row)
+__global__ void k_csr_rows(const int64_t* __restrict__ indptr, int n_bins,
+                           int32_t* __restrict__ row_of) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_bins) return;
+  for (int64_t j = indptr[i]; j < indptr[i + 1]; ++j) row_of[j] = i;
+}
+
+__global__ void k_union_keys(const int32_t* __restrict__ row_of,
+                             const int32_t* __restrict__ col,
+                             const double* __restrict__ val, int64_t n_ent,
+                             int64_t ent_offset, int rep, int R, int n_bins,
+                             int dist_max, const double* __restrict__ bias,
+                             int64_t sentinel, int64_t* __restrict__ keys,
+                             int32_t* __restrict__ ent_idx,
+                             int32_t* __restrict__ ent_rep,
+                             double* __restrict__ ent_val) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_ent;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int i = row_of[j];
+    const int c = col[j];
+    const double v = val[j];
+    const int d = c - i;
+    bool keep = (d >= 0) && (d <= dist_max) && (c < n_bins) && (v != 0.0);
+    if (keep) keep = bias[(int64_t)i * R + rep] != 0.0 && bias[(int64_t)c * R + rep] != 0.0;
+    const int64_t g = ent_offset + j;
+    keys[g] = keep ? (int64_t)i * n_bins + c : sentinel;
+    ent_idx[g] = (int32_t)g;
+    ent_rep[g] = rep;
+    ent_val[g] = v;
+  }
+}
+
+// head[i] = 1 where a new non-sentinel key starts
+__global__ void k_run_heads(const int64_t* __restrict__ keys, int64_t n,
+                            int64_t sentinel, int32_t* __restrict__ head) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[i];
+    head[i] = (k != sentinel && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+  }
+}
+
+// run starts: run r begins at the entry whose inclusive head-scan equals r+1
+__global__ void k_run_starts(const int32_t* __restrict__ head,
+                             const int32_t* __restrict__ run_incl, int64_t n,
+                             int64_t* __restrict__ run_start) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (head[i]) run_start[run_incl[i] - 1] = i;
+}
+
+// keep flag per run: deconvoluted sum finite and > 0
+__global__ void k_run_keep(const int64_t* __restrict__ keys,
+                           const int32_t* __restrict__ ent_sorted,
+                           const int64_t* __restrict__ run_start,
+                           int64_t n_runs, int64_t n_ent, int64_t sentinel,
+                           const int32_t* __restrict__ ent_rep,
+                           const double* __restrict__ ent_val, int R,
+                           int n_bins, const double* __restrict__ bias,
+                           int32_t* __restrict__ keep) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_runs;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = run_start[r];
+    const int64_t key = keys[b];
+    const int64_t i = key / n_bins, c = key - i * n_bins;
+    double tot = 0.0;
+    for (int64_t j = b; j < n_ent && keys[j] == key; ++j) {
+      const int e = ent_sorted[j];
+      const int rep = ent_rep[e];
+      const double bi = 1.0 / bias[i * R + rep], bc = 1.0 / bias[c * R + rep];
+      tot += (bi * ent_val[e]) * bc;
+    }
+    keep[r] = (tot > 0.0 && tot - tot == 0.0) ? 1 : 0;
+  }
+}
+
+// fill row/col/raw/balanced for kept runs (px = exclusive scan of keep)
+__global__ void k_union_fill(const int64_t* __restrict__ keys,
+                             const int32_t* __restrict__ ent_sorted,
+                             const int64_t* __restrict__ run_start,
+                             const int32_t* __restrict__ keep,
+                             const int32_t* __restrict__ px_incl,
+                             int64_t n_runs, int64_t n_ent,
+                             const int32_t* __restrict__ ent_rep,
+                             const double* __restrict__ ent_val, int R,
+                             int n_bins, const double* __restrict__ bias,
+                             int32_t* __restrict__ row, int32_t* __restrict__ col,
+                             int64_t* __restrict__ raw,
+                             double* __restrict__ balanced) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_runs;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    if (!keep[r]) continue;
+    const int64_t p = px_incl[r] - 1;
+    const int64_t b = run_start[r];
+    const int64_t key = keys[b];
+    const int64_t i = key / n_bins, c = key - i * n_bins;
+    row[p] = (int32_t)i;
+    col[p] = (int32_t)c;
+    for (int k = 0; k < R; ++k) {
+      raw[p * R + k] = 0;
+      balanced[p * R + k] = 0.0 / (bias[i * R + k] * bias[c * R + k]);
+    }
+    for (int64_t j = b; j < n_ent && keys[j] == key; ++j) {
+      const int e = ent_sorted[j];
+      const int k = ent_rep[e];
+      const double v = ent_val[e];
+      raw[p * R + k] = (int64_t)v;
+      balanced[p * R + k] = v / (bias[i * R + k] * bias[c * R + k]);
+    }
+  }
+}
+
+// ---- size factors ---------------------------------------------------------
+
+// equal_bin with the stable tie order: sorted position k -> bin
+// floor(k * (n_bins / n)) (numpy linspace(0, n_bins, n, endpoint=False,
+// dtype=int)); bin_of_sorted[k]
+__global__ void k_equal_bin(int64_t n, int n_bins, int32_t* __restrict__ bin) {
+  const double step = (double)n_bins / (double)n;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x)
+    bin[k] = (int32_t)floor((double)k * step);
+}
+
+// bin boundaries over the sorted positions: bin_start[b] = first k with
+// bin[k] >= b (b = 0..n_bins)
+__global__ void k_bin_bounds(const int32_t* __restrict__ bin, int64_t n,
+                             int n_bins, int64_t* __restrict__ bin_start) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > n_bins) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (bin[mid] < b)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  bin_start[b] = lo;
+}
+
+// ratio keys for the median: for sorted position k of bin b, replicate r:
+// data / gmean(data, pseudocount 1) when every replicate > 0 (scaling.py:44-47)
+// else +inf (sorts past the valid ones); valid rows counted per bin.
+__global__ void k_mor_keys(const double* __restrict__ balanced,
+                           const int32_t* __restrict__ perm, int64_t n, int R,
+                           const int32_t* __restrict__ bin,
+                           double* __restrict__ keys,
+                           int32_t* __restrict__ valid_per_bin) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = perm[k];
+    bool ok = true;
+    double s = 0.0;
+    for (int r = 0; r < R; ++r) {
+      const double v = balanced[i * R + r];
+      ok = ok && (v > 0.0);
+      s += log(v + 1);
+    }
+    const double gm = exp(s / R) - 1;
+    for (int r = 0; r < R; ++r)
+      keys[(int64_t)r * n + k] = ok ? balanced[i * R + r] / gm : INFINITY;
+    if (ok) atomicAdd(&valid_per_bin[bin[k]], 1);
+  }
+}
+
+// per (replicate, bin): median of the first `valid` sorted ratios; d_per_bin
+// = mean distance of the bin (exact: integer sum)
+__global__ void k_mor_median(const double* __restrict__ sorted_keys,
+                             const int64_t* __restrict__ bin_start,
+                             const int32_t* __restrict__ valid, int n_bins,
+                             int64_t n, int R, double* __restrict__ s_per_bin) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_bins * R) return;
+  const int b = t % n_bins, r = t / n_bins;
+  const int64_t base = (int64_t)r * n + bin_start[b];
+  const int64_t m = valid[b];
+  double med = NAN;
+  if (m > 0) {
+    if (m % 2)
+      med = sorted_keys[base + m / 2];
+    else
+      med = (sorted_keys[base + m / 2 - 1] + sorted_keys[base + m / 2]) / 2.0;
+  }
+  s_per_bin[(int64_t)b * R + r] = med;
+}
+
+__global__ void k_bin_dist_sum(const int32_t* __restrict__ dist_sorted,
+                               const int64_t* __restrict__ bin_start,
+                               int n_bins, double* __restrict__ d_per_bin) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_bins) return;
+  long long s = 0;
+  for (int64_t k = bin_start[b]; k < bin_start[b + 1]; ++k) s += dist_sorted[k];
+  const int64_t cnt = bin_start[b + 1] - bin_start[b];
+  d_per_bin[b] = cnt ? (double)s / (double)cnt : NAN;
+}
+
+// sf[i, r] = interp1d(d_per_bin, s_per_bin[:, r], extrapolate)(dist[i]) over
+// the non-empty bins (compacted by the host: m points)
+__global__ void k_sf_interp(const int32_t* __restrict__ dist, int64_t n, int R,
+                            const double* __restrict__ xp,
+                            const double* __restrict__ yp /* m x R */, int m,
+                            double* __restrict__ sf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = (double)dist[i];
+    int lo = 0, hi = m;  // lower_bound
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (xp[mid] < x)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    int idx = lo < 1 ? 1 : (lo > m - 1 ? m - 1 : lo);
+    const int a = idx - 1, b = idx;
+    for (int r = 0; r < R; ++r) {
+      const double slope = (yp[(int64_t)b * R + r] - yp[(int64_t)a * R + r]) / (xp[b] - xp[a]);
+      sf[i * R + r] = slope * (x - xp[a]) + yp[(int64_t)a * R + r];
+    }
+  }
+}
+
+// exact-distance mode: sf[i, r] = s_per_bin[bin(dist[i]), r]
+__global__ void k_sf_exact(const int32_t* __restrict__ perm,
+                           const int32_t* __restrict__ bin, int64_t n, int R,
+                           const double* __restrict__ s_per_bin,
+                           double* __restrict__ sf) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = perm[k];
+    for (int r = 0; r < R; ++r) sf[i * R + r] = s_per_bin[(int64_t)bin[k] * R + r];
+  }
+}
+
+// exact mode bins: bin of sorted position = its distance rank among distinct
+// distances (head flags scanned on device)
+__global__ void k_dist_heads(const int32_t* __restrict__ dist_sorted, int64_t n,
+                             int32_t* __restrict__ head) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x)
+    head[k] = (k == 0 || dist_sorted[k] != dist_sorted[k - 1]) ? 1 : 0;
+}
+
+__global__ void k_minus_one(int32_t* __restrict__ v, int64_t n) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x)
+    v[k] -= 1;
+}
+
+}  // namespace h3d

@@ -1,0 +1,265 @@
+// prepare_data entry points of libh3d.so (included at the end of
+// h3d_api.hip; shares its ctx / scratch / error helpers).
+#pragma once
+
+extern "C" {
+
+int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
+                    const int64_t* const* indptr, const int32_t* const* indices,
+                    const double* const* data, const int64_t* nnz,
+                    const double* bias, int dist_max, int64_t* n_px_out) {
+  if (!ctx || !indptr || !indices || !data || !nnz || !bias || !n_px_out)
+    return fail(H3D_EARG, "null argument");
+  if (R < 1 || R > kMaxReps || n_bins < 1 || dist_max < 0)
+    return fail(H3D_EARG, "R=%d n_bins=%d dist_max=%d", R, n_bins, dist_max);
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  PrepUnion& P = ctx->prep;
+  P = PrepUnion();
+  P.R = R;
+  P.n_bins = n_bins;
+  int64_t tot = 0;
+  for (int r = 0; r < R; ++r) {
+    if (nnz[r] < 0 || (nnz[r] > 0 && (!indices[r] || !data[r])) || !indptr[r])
+      return fail(H3D_EARG, "replicate %d CSR", r);
+    if (indptr[r][n_bins] != nnz[r]) return fail(H3D_EARG, "replicate %d indptr[-1] != nnz", r);
+    tot += nnz[r];
+  }
+  if (tot >= ((int64_t)1 << 31)) return fail(H3D_EARG, "too many entries");
+  P.n_entries = tot;
+  const int64_t sentinel = (int64_t)n_bins * n_bins;
+  int end_bit = 1;
+  while (end_bit < 63 && (((int64_t)1) << end_bit) <= sentinel) ++end_bit;
+  double* d_bias = (double*)scratch(ctx, "u_bias", (size_t)n_bins * R * 8);
+  int64_t* d_indptr = (int64_t*)scratch(ctx, "u_indptr", (size_t)(n_bins + 1) * 8);
+  int32_t* d_row = (int32_t*)scratch(ctx, "u_row_of", std::max<int64_t>(tot, 1) * 4);
+  int32_t* d_col = (int32_t*)scratch(ctx, "u_col", std::max<int64_t>(tot, 1) * 4);
+  double* d_val = (double*)scratch(ctx, "u_val_in", std::max<int64_t>(tot, 1) * 8);
+  int64_t* d_keys = (int64_t*)scratch(ctx, "u_keys", std::max<int64_t>(tot, 1) * 8);
+  int32_t* d_ent = (int32_t*)scratch(ctx, "u_ent", std::max<int64_t>(tot, 1) * 4);
+  P.keys_sorted = (int64_t*)scratch(ctx, "u_keys_s", std::max<int64_t>(tot, 1) * 8);
+  P.ent_sorted = (int32_t*)scratch(ctx, "u_ent_s", std::max<int64_t>(tot, 1) * 4);
+  P.ent_rep = (int32_t*)scratch(ctx, "u_ent_rep", std::max<int64_t>(tot, 1) * 4);
+  P.ent_val = (double*)scratch(ctx, "u_ent_val", std::max<int64_t>(tot, 1) * 8);
+  int32_t* d_head = (int32_t*)scratch(ctx, "u_head", std::max<int64_t>(tot, 1) * 4);
+  P.run_of = (int32_t*)scratch(ctx, "u_run_incl", std::max<int64_t>(tot, 1) * 4);
+  if (!d_bias || !d_indptr || !d_row || !d_col || !d_val || !d_keys || !d_ent ||
+      !P.keys_sorted || !P.ent_sorted || !P.ent_rep || !P.ent_val || !d_head || !P.run_of)
+    return fail(H3D_ENOMEM, "union scratch");
+  P.bias = d_bias;
+  HIP_TRY(hipMemcpyAsync(d_bias, bias, (size_t)n_bins * R * 8, hipMemcpyHostToDevice, s));
+  int64_t off = 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t m = nnz[r];
+    HIP_TRY(hipMemcpyAsync(d_indptr, indptr[r], (size_t)(n_bins + 1) * 8, hipMemcpyHostToDevice, s));
+    if (m > 0) {
+      HIP_TRY(hipMemcpyAsync(d_col, indices[r], m * 4, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(d_val, data[r], m * 8, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_csr_rows, dim3((n_bins + 255) / 256), dim3(256), 0, s,
+                         d_indptr, n_bins, d_row);
+      hipLaunchKernelGGL(k_union_keys, dim3(grid_for(ctx, m)), dim3(kBlock), 0, s,
+                         d_row, d_col, d_val, m, off, r, R, n_bins, dist_max, d_bias,
+                         sentinel, d_keys, d_ent, P.ent_rep, P.ent_val);
+    }
+    // the staging buffers are reused by the next replicate
+    HIP_TRY(hipStreamSynchronize(s));
+    off += m;
+  }
+  if (tot == 0) {
+    P.n_px = 0;
+    *n_px_out = 0;
+    return 0;
+  }
+  size_t tb = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_keys, P.keys_sorted, d_ent,
+                                             P.ent_sorted, (int)tot, 0, end_bit, s));
+  void* tmp = scratch(ctx, "cub_tmp_u", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_keys, P.keys_sorted, d_ent,
+                                             P.ent_sorted, (int)tot, 0, end_bit, s));
+  hipLaunchKernelGGL(k_run_heads, dim3(grid_for(ctx, tot)), dim3(kBlock), 0, s,
+                     P.keys_sorted, tot, sentinel, d_head);
+  tb = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_head, P.run_of, (int)tot, s));
+  tmp = scratch(ctx, "cub_tmp_s", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "scan temp");
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, P.run_of, (int)tot, s));
+  int32_t n_runs = 0;
+  HIP_TRY(hipMemcpyAsync(&n_runs, P.run_of + tot - 1, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  P.n_runs = n_runs;
+  P.run_start = (int64_t*)scratch(ctx, "u_run_start", std::max<int64_t>(n_runs, 1) * 8);
+  int32_t* keep = (int32_t*)scratch(ctx, "u_keep", std::max<int64_t>(n_runs, 1) * 4);
+  P.px_of_run = (int32_t*)scratch(ctx, "u_px_incl", std::max<int64_t>(n_runs, 1) * 4);
+  if (!P.run_start || !keep || !P.px_of_run) return fail(H3D_ENOMEM, "runs");
+  if (n_runs == 0) {
+    P.n_px = 0;
+    *n_px_out = 0;
+    return 0;
+  }
+  hipLaunchKernelGGL(k_run_starts, dim3(grid_for(ctx, tot)), dim3(kBlock), 0, s,
+                     d_head, P.run_of, tot, P.run_start);
+  hipLaunchKernelGGL(k_run_keep, dim3(grid_for(ctx, n_runs)), dim3(kBlock), 0, s,
+                     P.keys_sorted, P.ent_sorted, P.run_start, (int64_t)n_runs, tot,
+                     sentinel, P.ent_rep, P.ent_val, R, n_bins, d_bias, keep);
+  tb = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, keep, P.px_of_run, (int)n_runs, s));
+  tmp = scratch(ctx, "cub_tmp_s", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "scan temp");
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, P.px_of_run, (int)n_runs, s));
+  int32_t n_px = 0;
+  HIP_TRY(hipMemcpyAsync(&n_px, P.px_of_run + n_runs - 1, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  P.n_px = n_px;
+  *n_px_out = n_px;
+  return 0;
+}
+
+int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
+                   double* balanced, int64_t n_px) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  PrepUnion& P = ctx->prep;
+  if (n_px != P.n_px) return fail(H3D_EARG, "n_px %lld != counted %lld", (long long)n_px, (long long)P.n_px);
+  if (n_px == 0) return 0;
+  if (!row || !col || !raw || !balanced) return fail(H3D_EARG, "null output");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int R = P.R;
+  int32_t* d_row = (int32_t*)scratch(ctx, "u_out_row", n_px * 4);
+  int32_t* d_col = (int32_t*)scratch(ctx, "u_out_col", n_px * 4);
+  int64_t* d_raw = (int64_t*)scratch(ctx, "u_out_raw", n_px * R * 8);
+  double* d_bal = (double*)scratch(ctx, "u_out_bal", n_px * R * 8);
+  int32_t* keep = (int32_t*)scratch(ctx, "u_keep", std::max<int64_t>(P.n_runs, 1) * 4);
+  if (!d_row || !d_col || !d_raw || !d_bal) return fail(H3D_ENOMEM, "union out");
+  hipLaunchKernelGGL(k_union_fill, dim3(grid_for(ctx, P.n_runs)), dim3(kBlock), 0, s,
+                     P.keys_sorted, P.ent_sorted, P.run_start, keep, P.px_of_run,
+                     P.n_runs, P.n_entries, P.ent_rep, P.ent_val, R, P.n_bins, P.bias,
+                     d_row, d_col, d_raw, d_bal);
+  HIP_TRY(hipMemcpyAsync(row, d_row, n_px * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(col, d_col, n_px * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(raw, d_raw, n_px * R * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(balanced, d_bal, n_px * R * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
+                          const int32_t* dist, int64_t n, int R, int n_bins,
+                          double* sf_out) {
+  if (!ctx || (n > 0 && (!balanced || !dist || !sf_out))) return fail(H3D_EARG, "null argument");
+  if (R < 1 || R > kMaxReps || n_bins < 0) return fail(H3D_EARG, "R=%d n_bins=%d", R, n_bins);
+  if (n == 0) return 0;
+  if (n >= ((int64_t)1 << 31) / R) return fail(H3D_EARG, "n too large");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  double* d_bal = (double*)scratch(ctx, "sf_bal", n * R * 8);
+  int32_t* d_dist = (int32_t*)scratch(ctx, "sf_dist", n * 4);
+  int32_t* d_dist_s = (int32_t*)scratch(ctx, "sf_dist_s", n * 4);
+  int32_t* d_idx = (int32_t*)scratch(ctx, "sf_idx", n * 4);
+  int32_t* d_perm = (int32_t*)scratch(ctx, "sf_perm", n * 4);
+  int32_t* d_bin = (int32_t*)scratch(ctx, "sf_bin", n * 4);
+  double* d_keys = (double*)scratch(ctx, "sf_keys", n * R * 8);
+  double* d_keys_s = (double*)scratch(ctx, "sf_keys_s", n * R * 8);
+  double* d_sf = (double*)scratch(ctx, "sf_out", n * R * 8);
+  if (!d_bal || !d_dist || !d_dist_s || !d_idx || !d_perm || !d_bin || !d_keys ||
+      !d_keys_s || !d_sf)
+    return fail(H3D_ENOMEM, "size factor scratch");
+  HIP_TRY(hipMemcpyAsync(d_bal, balanced, n * R * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
+  // stable sort by distance (the pinned equal_bin tie order)
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_idx, n);
+  size_t tb = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_dist, d_dist_s, d_idx, d_perm,
+                                             (int)n, 0, 31, s));
+  void* tmp = scratch(ctx, "cub_tmp_sf", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_dist, d_dist_s, d_idx, d_perm,
+                                             (int)n, 0, 31, s));
+  int nb = n_bins;
+  if (n_bins > 0) {
+    hipLaunchKernelGGL(k_equal_bin, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, n,
+                       n_bins, d_bin);
+  } else {
+    int32_t* d_head = (int32_t*)scratch(ctx, "sf_head", n * 4);
+    if (!d_head) return fail(H3D_ENOMEM, "heads");
+    hipLaunchKernelGGL(k_dist_heads, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                       d_dist_s, n, d_head);
+    tb = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_head, d_bin, (int)n, s));
+    tmp = scratch(ctx, "cub_tmp_s", tb);
+    if (!tmp) return fail(H3D_ENOMEM, "scan temp");
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, d_bin, (int)n, s));
+    hipLaunchKernelGGL(k_minus_one, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bin, n);
+    int32_t last = 0;
+    HIP_TRY(hipMemcpyAsync(&last, d_bin + n - 1, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    nb = last + 1;
+  }
+  int64_t* d_bstart = (int64_t*)scratch(ctx, "sf_bstart", (size_t)(nb + 1) * 8);
+  int32_t* d_valid = (int32_t*)scratch(ctx, "sf_valid", (size_t)nb * 4);
+  double* d_spb = (double*)scratch(ctx, "sf_spb", (size_t)nb * R * 8);
+  double* d_dpb = (double*)scratch(ctx, "sf_dpb", (size_t)nb * 8);
+  int64_t* d_segb = (int64_t*)scratch(ctx, "sf_segb", (size_t)nb * R * 8);
+  int64_t* d_sege = (int64_t*)scratch(ctx, "sf_sege", (size_t)nb * R * 8);
+  if (!d_bstart || !d_valid || !d_spb || !d_dpb || !d_segb || !d_sege)
+    return fail(H3D_ENOMEM, "bins");
+  hipLaunchKernelGGL(k_bin_bounds, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_bin,
+                     n, nb, d_bstart);
+  HIP_TRY(hipMemsetAsync(d_valid, 0, (size_t)nb * 4, s));
+  hipLaunchKernelGGL(k_mor_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bal,
+                     d_perm, n, R, d_bin, d_keys, d_valid);
+  std::vector<int64_t> bstart(nb + 1);
+  HIP_TRY(hipMemcpyAsync(bstart.data(), d_bstart, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<int64_t> segb((size_t)nb * R), sege((size_t)nb * R);
+  for (int r = 0; r < R; ++r)
+    for (int b = 0; b < nb; ++b) {
+      segb[(size_t)r * nb + b] = (int64_t)r * n + bstart[b];
+      sege[(size_t)r * nb + b] = (int64_t)r * n + bstart[b + 1];
+    }
+  HIP_TRY(hipMemcpyAsync(d_segb, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_sege, sege.data(), sege.size() * 8, hipMemcpyHostToDevice, s));
+  tb = 0;
+  HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, d_keys, d_keys_s,
+                                                     (int)(n * R), nb * R, d_segb, d_sege,
+                                                     0, 64, s));
+  tmp = scratch(ctx, "cub_tmp_seg", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "segmented sort temp");
+  HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tb, d_keys, d_keys_s,
+                                                     (int)(n * R), nb * R, d_segb, d_sege,
+                                                     0, 64, s));
+  hipLaunchKernelGGL(k_mor_median, dim3((nb * R + 255) / 256), dim3(256), 0, s, d_keys_s,
+                     d_bstart, d_valid, nb, n, R, d_spb);
+  if (n_bins > 0) {
+    hipLaunchKernelGGL(k_bin_dist_sum, dim3((nb + 255) / 256), dim3(256), 0, s, d_dist_s,
+                       d_bstart, nb, d_dpb);
+    std::vector<double> dpb(nb), spb((size_t)nb * R);
+    HIP_TRY(hipMemcpyAsync(dpb.data(), d_dpb, nb * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(spb.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // np.unique(bins): only non-empty bins take part in the interpolation
+    std::vector<double> xp, yp;
+    for (int b = 0; b < nb; ++b)
+      if (bstart[b + 1] > bstart[b]) {
+        xp.push_back(dpb[b]);
+        for (int r = 0; r < R; ++r) yp.push_back(spb[(size_t)b * R + r]);
+      }
+    const int m = (int)xp.size();
+    if (m < 2) return fail(H3D_EARG, "fewer than two distance bins to interpolate");
+    double* d_xp = (double*)scratch(ctx, "sf_xp", m * 8);
+    double* d_yp = (double*)scratch(ctx, "sf_yp", (size_t)m * R * 8);
+    if (!d_xp || !d_yp) return fail(H3D_ENOMEM, "interp");
+    HIP_TRY(hipMemcpyAsync(d_xp, xp.data(), m * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_yp, yp.data(), (size_t)m * R * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_sf_interp, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_dist, n,
+                       R, d_xp, d_yp, m, d_sf);
+  } else {
+    hipLaunchKernelGGL(k_sf_exact, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_perm,
+                       d_bin, n, R, d_spb, d_sf);
+  }
+  HIP_TRY(hipMemcpyAsync(sf_out, d_sf, n * R * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+/* h3d.h — C ABI of libh3d.so, the MI355X-native hot path of hic3defdr.
+ *
+ * The reference (thomasgilgenast/hic3defdr 0.2.1) is pure Python and has no
+ * FFI; this ABI sits behind its operator-level functions, which the Python
+ * mirror (hic3defdr_amd) binds with ctypes:
+ *
+ *   h3d_union_*            <- util/matrices.py:92-129 sparse_union (+ the raw /
+ *                              balanced gathers, analysis/analysis.py:91-101)
+ *   h3d_size_factors_cmor  <- util/scaling.py:108-127 conditional_mor
+ *   h3d_disp_per_dist      <- analysis/analysis.py:185-206 (estimator per
+ *                              distance/condition; util/dispersion.py:10-80
+ *                              qcml/cml, util/scaled_nb.py:71-275)
+ *   h3d_disp_table         <- analysis/analysis.py:208-218 +
+ *                              util/lowess.py:10-244 (the fitted disp_fn,
+ *                              tabulated on every integer distance)
+ *   h3d_lrt                <- util/lrt.py:7-50 (+ analysis/analysis.py:272-278)
+ *   h3d_bh                 <- analysis/analysis.py:286-303 (lib5c
+ *                              adjust_pvalues = BH)
+ *
+ * Conventions: 0 on success, a negative H3D_E* code otherwise (the message is
+ * in h3d_last_error(), thread-local). Host buffers are C-contiguous and owned
+ * by the caller; device buffers of the *_dev entry points are device pointers
+ * the caller owns. Calls are synchronous unless they take a stream. One ctx
+ * per device; a ctx is not shared between threads.
+ */
+#ifndef H3D_H_
+#define H3D_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H3D_OK 0
+#define H3D_EARG (-1)    /* bad argument: null pointer, size, shape        */
+#define H3D_EHIP (-2)    /* HIP runtime error                               */
+#define H3D_ENOCONV (-3) /* numerical failure the reference raises on      */
+#define H3D_ENOMEM (-4)  /* device allocation failed                       */
+#define H3D_EINPUT (-5)  /* invalid numeric input (reference asserts)      */
+#define H3D_ENODEV (-6)  /* no usable gfx950 device                        */
+
+#define H3D_EST_QCML 0
+#define H3D_EST_CML 1
+#define H3D_EST_MME 2
+
+/* per-segment / per-pixel status bits (also in *flags outputs) */
+#define H3D_FLAG_NOROOT 1   /* all-zero counts: no MLE (ref ValueError)      */
+#define H3D_FLAG_NOCONV 2   /* MLE solver did not converge                   */
+#define H3D_FLAG_BRENT 4    /* bounded Brent failed (ref assert res.success) */
+#define H3D_FLAG_QGUARD 8   /* qcml did not converge in 1000 iterations      */
+#define H3D_FLAG_BADIN 16   /* alpha/b not positive finite (ref assert)      */
+
+typedef struct h3d_ctx h3d_ctx;
+
+/* All-reduce hook for multi-GPU estimate_disp: called between data passes
+ * with a DEVICE buffer of `count` doubles that must be summed in place across
+ * ranks on the ctx stream (e.g. torch.distributed.all_reduce over RCCL).
+ * Return 0 on success. */
+typedef int (*h3d_allreduce_fn)(double* dev_buf, int64_t count, void* user);
+
+int h3d_version(void);
+int h3d_device_count(void);
+h3d_ctx* h3d_open(int device);
+void h3d_close(h3d_ctx* ctx);
+const char* h3d_last_error(void);
+/* stream the ctx launches on (hipStream_t); NULL = the ctx's own stream */
+int h3d_set_stream(h3d_ctx* ctx, void* stream);
+
+/* ---- prepare_data ------------------------------------------------------ */
+
+/* Union pixel set of R upper-triangular CSR replicate matrices restricted to
+ * 0 <= col-row <= dist_max and to bins whose bias is non-zero in every
+ * replicate (matrices.py:92-129 with deconvolute(invert=True)). Two-pass:
+ * count, then fill. indptr[r] has n_bins+1 entries, indices[r]/data[r] nnz[r].
+ * bias is (n_bins, R) row-major and already bias_thresh-filtered
+ * (core.py:35-60). */
+int h3d_union_count(h3d_ctx* ctx, int R, int n_bins, const int64_t* const* indptr,
+                    const int32_t* const* indices, const double* const* data,
+                    const int64_t* nnz, const double* bias, int dist_max,
+                    int64_t* n_px_out);
+/* row/col (n_px), raw (n_px, R) int64 = summed counts, balanced (n_px, R) =
+ * raw / (bias[row, r] * bias[col, r]) (analysis.py:91-101). */
+int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
+                   double* balanced, int64_t n_px);
+
+/* Distance-conditional median-of-ratios size factors (scaling.py:68-127) with
+ * n_bins equal-number distance bins (stable tie order), or
+ * exact distances when n_bins == 0. balanced (n, R), dist (n) -> sf (n, R). */
+int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
+                          const int32_t* dist, int64_t n, int R, int n_bins,
+                          double* sf_out);
+
+/* ---- estimate_disp ----------------------------------------------------- */
+
+/* Per-(distance, condition) dispersion (analysis.py:185-206). raw/f (n, R),
+ * dist (n) in [0, D); cond_of_rep (R) in [0, C). Output disp_per_dist (D, C)
+ * (NaN for empty slices), seg_flags (D, C) optional. */
+int h3d_disp_per_dist(h3d_ctx* ctx, const int64_t* raw, const double* f,
+                      const int32_t* dist, int64_t n, int R, int C,
+                      const int32_t* cond_of_rep, int D, int estimator,
+                      double* disp_per_dist, int32_t* seg_flags);
+
+/* Same on device-resident inputs: d_raw (n, R) int32, d_f (n, R), d_dist (n).
+ * `reduce` (optional) makes the per-segment sums global across ranks; every
+ * rank must pass the same D, C, cond_of_rep. */
+int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                          const int32_t* d_dist, int64_t n, int R, int C,
+                          const int32_t* cond_of_rep, int D, int estimator,
+                          double* disp_per_dist, int32_t* seg_flags,
+                          h3d_allreduce_fn reduce, void* user);
+
+/* Smoothed dispersion function of one condition, tabulated at d = 0..D-1
+ * (lowess.py:95-244 weighted_lowess_fit if weighted, else lowess_fit;
+ * left_boundary = first finite value, as analysis.py:212). frac < 0 = auto. */
+int h3d_disp_table(const double* disp_per_dist_col, int D, int weighted,
+                   double frac, double auto_frac_factor, double* table_out);
+
+/* ---- lrt --------------------------------------------------------------- */
+
+/* Per-pixel LRT (lrt.py:7-50) with disp[i, c] = disp_table[dist[i], c]
+ * (disp_table (D, C)); with dist == NULL, disp_table is the per-pixel
+ * dispersion array (n, C) itself (the reference's disp_<chrom>.npy, as
+ * analysis.py:269-278 loads it). Outputs p, llr, mu0 (n), mu1 (n, C);
+ * disp_out (n, C) optional. */
+int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
+            const int32_t* dist, const double* disp_table, int64_t n, int R,
+            int C, const int32_t* cond_of_rep, int D, int refit_mu, double* p,
+            double* llr, double* mu0, double* mu1, double* disp_out);
+
+int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                const int32_t* d_dist, const double* disp_table, int64_t n,
+                int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
+                double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
+                double* d_disp);
+
+/* ---- bh ---------------------------------------------------------------- */
+
+/* Benjamini-Hochberg q-values over the finite p-values (NaN elsewhere). */
+int h3d_bh(const double* p, int64_t n, double* q);
+
+/* ---- measurement -------------------------------------------------------- */
+
+/* Per-kernel HIP-event timing on the ctx stream. name in {"disp_work",
+ * "disp_reduce", "disp_update", "disp_prep", "lrt"}. */
+int h3d_profile_enable(h3d_ctx* ctx, int on);
+int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
+                     int64_t* launches, int64_t* units);
+int h3d_profile_reset(h3d_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* H3D_H_ */

@@ -545,8 +545,10 @@ def lowess_fit(x, y, logx=False, logy=False, left_boundary=None,
 def weighted_lowess_fit(x, y, logx=False, logy=False, left_boundary=None,
                         right_boundary=None, frac=None, auto_frac_factor=15.,
                         delta=0.01, w=20, power=1. / 4,
-                        interpolate_before_increase=True):
-    """``lowess.py:95-244``."""
+                        interpolate_before_increase=True,
+                        intended_min_weight=True):
+    """``lowess.py:95-244``. ``intended_min_weight=False`` is the reference
+    bit for bit; True pins the smallest scaled weight to exactly 1."""
     n = len(y)
     i = np.arange(n)
     sort_idx = np.argsort(x)
@@ -559,6 +561,10 @@ def weighted_lowess_fit(x, y, logx=False, logy=False, left_boundary=None,
     weight[np.isfinite(prec)] = np.power(prec[np.isfinite(prec)], power)
     min_weight = np.nanmin(weight)
     scaled_weight = weight * (1 / min_weight)
+    if intended_min_weight:
+        # pinned deviation shared with libh3d: w * (1/w) rounds
+        # to 1 - 2^-53 for ~13% of w and floor() would drop the point
+        scaled_weight[weight == min_weight] = 1.0
     max_weight = np.nanmax(scaled_weight)
     scaled_weight[np.isinf(scaled_weight)] = max_weight
     left_weight = scaled_weight[np.argmax(np.isfinite(scaled_weight))]

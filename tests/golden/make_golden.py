@@ -102,6 +102,9 @@ def run_e2e(name):
     for c, cond in enumerate(kw['conds']):
         fn = h.load_disp_fn(cond)
         out['disp_fn_table__%s' % cond] = fn(np.arange(dmax + 1))
+        xs = np.linspace(-3.0, dmax + 25.0, 997)
+        out['disp_fn_xs'] = xs
+        out['disp_fn_cont__%s' % cond] = fn(xs)
     np.savez_compressed(os.path.join(HERE, 'e2e_%s.npz' % name), **out)
     print(name, 'pixels', sum(len(out['row__%s' % c]) for c in kw['chroms']),
           'disp px', sum(len(out['pvalues__%s' % c]) for c in kw['chroms']))

@@ -1,0 +1,138 @@
+"""GPU parity: libh3d.so kernels on a real MI355X vs the reference goldens and
+the CPU oracle. Tolerances (north star): p/q within 1e-6 relative; integer
+outputs (union pixels, raw counts, disp_idx, loop_idx) bit-exact."""
+import numpy as np
+import pytest
+import scipy.sparse as sparse
+
+import oracle
+from conftest import e2e_inputs, rel_err
+
+pytestmark = pytest.mark.gpu
+
+RTOL_PQ = 1e-6      # north-star tolerance on p- and q-values
+RTOL_DISP = 1e-6    # per-distance qcml (Brent xatol 1e-5 on a flat NLL)
+RTOL_MU = 1e-8      # MLE of mu (reference secant tol 1.48e-8 absolute)
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from hic3defdr_amd import _native
+    return _native.context(0)
+
+
+def _stage_inputs(name):
+    """raw / f / dist of the disp pixels exactly as the reference's
+    estimate_disp builds them (analysis.py:169-183), from the goldens."""
+    g, kw = e2e_inputs(name)
+    raws, fs, dists = [], [], []
+    for c in kw['chroms']:
+        bias = oracle.load_bias([p.replace('<chrom>', c)
+                                 for p in kw['bias_patterns']])
+        di = g['disp_idx__%s' % c]
+        row, col = g['row__%s' % c][di], g['col__%s' % c][di]
+        raws.append(g['raw__%s' % c][di])
+        fs.append(bias[row] * bias[col] * g['size_factors__%s' % c][di])
+        dists.append(col - row)
+    return g, kw, np.concatenate(raws), np.concatenate(fs), \
+        np.concatenate(dists)
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+def test_disp_per_dist_vs_reference(ctx, name):
+    g, kw, raw, f, dist = _stage_inputs(name)
+    design = kw['design']
+    C = design.shape[1]
+    D = kw['dist_thresh_max'] + 1
+    out = ctx.disp_per_dist(raw, f, dist, design.argmax(axis=1), C, D)
+    ref = g['disp_per_dist']
+    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+    np.testing.assert_allclose(out, ref, rtol=RTOL_DISP, atol=1e-12)
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+def test_lrt_vs_reference(ctx, name):
+    from hic3defdr_amd import _native
+    g, kw, raw, f, dist = _stage_inputs(name)
+    design = kw['design']
+    tab = np.stack([_native.disp_table(g['disp_per_dist'][:, c])
+                    for c in range(design.shape[1])], axis=1)
+    p, llr, m0, m1, disp = ctx.lrt(raw, f, dist, tab, design.argmax(axis=1))
+    pr = np.concatenate([g['pvalues__%s' % c] for c in kw['chroms']])
+    m0r = np.concatenate([g['mu_hat_null__%s' % c] for c in kw['chroms']])
+    m1r = np.concatenate([g['mu_hat_alt__%s' % c] for c in kw['chroms']])
+    dr = np.concatenate([g['disp__%s' % c] for c in kw['chroms']])
+    assert rel_err(disp, dr) < 1e-12
+    assert rel_err(p, pr) < RTOL_PQ
+    assert rel_err(m0, m0r) < RTOL_MU
+    assert rel_err(m1, m1r) < RTOL_MU
+
+
+def test_lrt_refit_false_vs_oracle(ctx):
+    g, kw, raw, f, dist = _stage_inputs('small2')
+    design = kw['design']
+    from hic3defdr_amd import _native
+    tab = np.stack([_native.disp_table(g['disp_per_dist'][:, c])
+                    for c in range(design.shape[1])], axis=1)
+    p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, design.argmax(axis=1),
+                                refit_mu=False)
+    disp = tab[dist]
+    rp, rllr, rm0, rm1 = oracle.lrt(raw, f, np.dot(disp, design.T), design,
+                                    refit_mu=False)
+    assert rel_err(p, rp) < RTOL_PQ
+    assert rel_err(m0, rm0) < 1e-14
+    assert rel_err(m1, rm1) < 1e-14
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+def test_union_and_size_factors_vs_reference(ctx, name):
+    g, kw = e2e_inputs(name)
+    for c in kw['chroms']:
+        bias = oracle.load_bias([p.replace('<chrom>', c)
+                                 for p in kw['bias_patterns']])
+        mats = []
+        for p in kw['raw_npz_patterns']:
+            m = sparse.load_npz(p.replace('<chrom>', c)).tocsr()
+            m.sum_duplicates()
+            mats.append(m)
+        row, col, raw, bal = ctx.sparse_union(mats, bias,
+                                              kw['dist_thresh_max'])
+        np.testing.assert_array_equal(row, g['row__%s' % c])
+        np.testing.assert_array_equal(col, g['col__%s' % c])
+        np.testing.assert_array_equal(raw, g['raw__%s' % c])
+        nb = int(kw['dist_thresh_max'] / 5)
+        sf = ctx.size_factors_cmor(bal, col - row, nb)
+        assert rel_err(sf, g['size_factors__%s' % c]) < 1e-13
+        sf0 = ctx.size_factors_cmor(bal, col - row, 0)
+        assert rel_err(sf0, oracle.conditional_mor(bal, col - row)) < 1e-13
+
+
+def test_disp_and_lrt_vs_oracle_larger(ctx):
+    """A 900-bin synthetic chromosome: GPU vs the CPU oracle end to end from
+    the same prepared inputs (the oracle finishes in seconds)."""
+    import tempfile
+    from hic3defdr_amd import synthetic, _native
+    with tempfile.TemporaryDirectory() as tmp:
+        kw = synthetic.write_dataset(tmp, {'chrX': 900}, dist_thresh_max=80,
+                                     seed=7)
+        design = kw['design']
+        chrom = 'chrX'
+        npz = [p.replace('<chrom>', chrom) for p in kw['raw_npz_patterns']]
+        bfs = [p.replace('<chrom>', chrom) for p in kw['bias_patterns']]
+        prep = oracle.prepare_chrom(npz, bfs, design, dist_thresh_max=80)
+        bias = oracle.load_bias(bfs)
+        di = prep['disp_idx']
+        row, col = prep['row'][di], prep['col'][di]
+        raw = prep['raw'][di]
+        f = bias[row] * bias[col] * prep['size_factors'][di]
+        dist = col - row
+        disp, dpd, _ = oracle.estimate_disp([prep], [bias], design,
+                                            dist_thresh_max=80)
+        out = ctx.disp_per_dist(raw, f, dist, design.argmax(axis=1), 2, 81)
+        np.testing.assert_allclose(out, dpd, rtol=RTOL_DISP, atol=1e-12)
+        tab = np.stack([_native.disp_table(out[:, c]) for c in range(2)],
+                       axis=1)
+        p, llr, m0, m1, d = ctx.lrt(raw, f, dist, tab, design.argmax(axis=1))
+        rp, _, rm0, rm1 = oracle.lrt(raw, f, np.dot(disp, design.T), design)
+        assert rel_err(p, rp) < RTOL_PQ
+        assert rel_err(m0, rm0) < RTOL_MU
