@@ -62,6 +62,8 @@ struct h3d_ctx {
   std::map<std::string, std::pair<void*, size_t>> bufs;
   // prepare_data state between h3d_union_count and h3d_union_fill
   PrepUnion prep;
+  // [equalize, nll] pixel-replicates processed by disp_work (measurement)
+  unsigned long long* work_count = nullptr;
 };
 
 namespace {
@@ -162,7 +164,18 @@ void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
                       const int32_t* list_len, double* partial) {
   hipLaunchKernelGGL(k_disp_work<M>, dim3(grid), dim3(kBlock), 0, ctx->stream,
                      raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
-                     seg_flags, list, list_len, partial);
+                     seg_flags, list, list_len, partial, ctx->work_count);
+}
+
+// algorithmic HBM bytes of the disp_work launches so far: an equalize
+// pixel-replicate reads raw (4 B) + f (8 B) and writes pseudodata (8 B); an
+// NLL pixel-replicate reads pseudodata (8 B)
+int64_t disp_work_bytes(h3d_ctx* ctx) {
+  unsigned long long c[2] = {0, 0};
+  if (!ctx->work_count) return 0;
+  (void)hipMemcpyAsync(c, ctx->work_count, sizeof(c), hipMemcpyDeviceToHost, ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream);
+  return (int64_t)(c[0] * 20ull + c[1] * 8ull);
 }
 
 template <int M, int CM>
@@ -230,6 +243,13 @@ h3d_ctx* h3d_open(int device) {
     return nullptr;
   }
   ctx->stream = ctx->own;
+  if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
+    (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    fail(H3D_ENOMEM, "counter allocation failed");
+    return nullptr;
+  }
   return ctx;
 }
 
@@ -241,6 +261,7 @@ void h3d_close(h3d_ctx* ctx) {
   for (auto& kv : ctx->bufs)
     if (kv.second.first) (void)hipFree(kv.second.first);
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  if (ctx->work_count) (void)hipFree(ctx->work_count);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -262,6 +283,8 @@ int h3d_profile_reset(h3d_ctx* ctx) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   prof_collect(ctx);
   ctx->stats.clear();
+  HIP_TRY(hipMemsetAsync(ctx->work_count, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 
@@ -273,7 +296,8 @@ int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
   ProfEntry e = (it == ctx->stats.end()) ? ProfEntry() : it->second;
   if (total_ms) *total_ms = e.ms;
   if (launches) *launches = e.launches;
-  if (units) *units = e.units;
+  // disp_work units = algorithmic bytes; lrt / disp_prep units = pixels
+  if (units) *units = std::strcmp(name, "disp_work") == 0 ? disp_work_bytes(ctx) : e.units;
   return 0;
 }
 

@@ -130,4 +130,61 @@ double h3dt_qcml(int64_t n, int r, const int32_t* x, const double* f,
   return st.result;
 }
 
+// Host emulation of the multi-rank estimate_disp driver (h3d_disp_per_dist_dev
+// with an all-reduce hook): this rank's pixels, stable-ordered by distance;
+// per data pass every active segment's local NLL total, summed across ranks
+// by `reduce`, then the shared qcml/Brent state machines advance. Used by the
+// gloo world_size-2 tests to check the sharded algorithm on CPU.
+typedef int (*h3dt_reduce_fn)(double* buf, int64_t count, void* user);
+
+int h3dt_disp_rounds(int64_t n, int R, int C, const int32_t* raw,
+                     const double* f, const int32_t* dist,
+                     const int32_t* cond_of_rep, int D, h3dt_reduce_fn reduce,
+                     void* user, double* out, int32_t* flags_out) {
+  const int S = D * C;
+  std::vector<int> nrep(C, 0), rep_idx(C * M, 0);
+  for (int r = 0; r < R; ++r) rep_idx[cond_of_rep[r] * M + nrep[cond_of_rep[r]]++] = r;
+  std::vector<std::vector<int64_t>> px(D);
+  for (int64_t i = 0; i < n; ++i) px[dist[i]].push_back(i);
+  std::vector<double> cnt(S, 0.0), tot(S, 0.0);
+  for (int d = 0; d < D; ++d)
+    for (int c = 0; c < C; ++c) cnt[d * C + c] = (double)px[d].size();
+  if (reduce && reduce(cnt.data(), S, user)) return -2;
+  std::vector<h3d::SegState> st(S);
+  for (int s = 0; s < S; ++s) h3d::seg_init(&st[s], (long long)cnt[s], nrep[s % C]);
+  std::vector<double> pd((size_t)n * R, 0.0);
+  for (int guard = 0; guard < 200000; ++guard) {
+    bool any = false;
+    for (int s = 0; s < S; ++s) any |= st[s].phase != h3d::kDone;
+    if (!any) break;
+    for (int s = 0; s < S; ++s) {
+      tot[s] = 0.0;
+      if (st[s].phase == h3d::kDone) continue;
+      const int d = s / C, c = s % C, nr = nrep[c];
+      for (int64_t i : px[d]) {
+        double x[M], fv[M], dd[M];
+        for (int k = 0; k < nr; ++k) {
+          const int r = rep_idx[c * M + k];
+          x[k] = raw[i * R + r];
+          fv[k] = f[i * R + r];
+          dd[k] = pd[i * R + r];
+        }
+        if (st[s].phase == h3d::kEqualize) {
+          st[s].flags |= h3d::equalize_pixel<M>(x, fv, nr, st[s].disp, dd);
+          for (int k = 0; k < nr; ++k) pd[i * R + rep_idx[c * M + k]] = dd[k];
+        }
+        tot[s] += h3d::nll_pixel<M>(dd, nr, st[s].k);
+      }
+    }
+    if (reduce && reduce(tot.data(), S, user)) return -2;
+    for (int s = 0; s < S; ++s)
+      if (st[s].phase != h3d::kDone) h3d::seg_step(&st[s], tot[s], nrep[s % C]);
+  }
+  for (int s = 0; s < S; ++s) {
+    out[s] = st[s].result;
+    if (flags_out) flags_out[s] = st[s].flags;
+  }
+  return 0;
+}
+
 }  // extern "C"

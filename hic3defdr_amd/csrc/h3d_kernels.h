@@ -101,7 +101,8 @@ __global__ __launch_bounds__(kBlock) void k_disp_work(
     int C, const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
     const int32_t* __restrict__ n_rep /* C */, const SegState* __restrict__ st,
     int* __restrict__ seg_flags, const int32_t* __restrict__ list,
-    const int32_t* __restrict__ list_len, double* __restrict__ partial) {
+    const int32_t* __restrict__ list_len, double* __restrict__ partial,
+    unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
   __shared__ double lds[kBlock / 64];
   const int len = *list_len;
   for (int w = blockIdx.x; w < len; w += gridDim.x) {
@@ -110,6 +111,9 @@ __global__ __launch_bounds__(kBlock) void k_disp_work(
     const int s = chunk_d[chunk] * C + c;
     const int phase = st[s].phase;
     const int nr = n_rep[c];
+    if (threadIdx.x == 0)
+      atomicAdd(&work_count[phase == kEqualize ? 0 : 1],
+                (unsigned long long)chunk_len[chunk] * nr);
     double term = 0.0;
     const int i = threadIdx.x;
     if (i < chunk_len[chunk]) {
