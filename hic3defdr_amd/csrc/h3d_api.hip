@@ -64,6 +64,11 @@ struct h3d_ctx {
   PrepUnion prep;
   // [equalize, nll] pixel-replicates processed by disp_work (measurement)
   unsigned long long* work_count = nullptr;
+  // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
+  // disp_work register budget (1, 3, 4); H3D_DISP_SORT = 0 (distance) or
+  // 1 (distance, total count)
+  int disp_w = 4;     // measured best (r01 sweep: 1 / 3 / 4 -> 52.5 / 53.5 / 50.4 ms)
+  int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
 };
 
 namespace {
@@ -162,9 +167,18 @@ void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
                       int C, const int32_t* rep_idx, const int32_t* n_rep,
                       const SegState* st, int* seg_flags, const int32_t* list,
                       const int32_t* list_len, double* partial) {
-  hipLaunchKernelGGL(k_disp_work<M>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                     raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
-                     seg_flags, list, list_len, partial, ctx->work_count);
+  if (M == 4 && ctx->disp_w == 4)
+    hipLaunchKernelGGL((k_disp_work<M, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
+                       seg_flags, list, list_len, partial, ctx->work_count);
+  else if (M == 4 && ctx->disp_w == 3)
+    hipLaunchKernelGGL((k_disp_work<M, 3>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
+                       seg_flags, list, list_len, partial, ctx->work_count);
+  else
+    hipLaunchKernelGGL((k_disp_work<M, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
+                       seg_flags, list, list_len, partial, ctx->work_count);
 }
 
 // algorithmic HBM bytes of the disp_work launches so far: an equalize
@@ -243,6 +257,8 @@ h3d_ctx* h3d_open(int device) {
     return nullptr;
   }
   ctx->stream = ctx->own;
+  if (const char* e = std::getenv("H3D_DISP_W")) ctx->disp_w = std::atoi(e);
+  if (const char* e = std::getenv("H3D_DISP_SORT")) ctx->disp_sort = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
@@ -343,12 +359,30 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     int end_bit = 1;
     while ((1 << end_bit) <= D) ++end_bit;
     size_t tmp_bytes = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_dist, dist_s,
-                                               idx_in, idx_out, (int)n, 0, end_bit, s));
-    void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
-    if (!tmp) return fail(H3D_ENOMEM, "sort temp");
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
-                                               idx_out, (int)n, 0, end_bit, s));
+    if (ctx->disp_sort == 1) {
+      // (distance, total count) keys: same segments, less lane divergence
+      uint64_t* keys = (uint64_t*)scratch(ctx, "dkeys", n * 8);
+      uint64_t* keys_s = (uint64_t*)scratch(ctx, "dkeys_s", n * 8);
+      if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
+      hipLaunchKernelGGL(k_dist_count_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         d_dist, d_raw, n, R, keys);
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s,
+                                                 idx_in, idx_out, (int)n, 0,
+                                                 32 + end_bit, s));
+      void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+      if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_s, idx_in,
+                                                 idx_out, (int)n, 0, 32 + end_bit, s));
+      hipLaunchKernelGGL(k_key_dist, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         keys_s, n, dist_s);
+    } else {
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_dist, dist_s,
+                                                 idx_in, idx_out, (int)n, 0, end_bit, s));
+      void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+      if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
+                                                 idx_out, (int)n, 0, end_bit, s));
+    }
     hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
                        idx_out, d_raw, d_f, n, R, raw_s, f_s);
     hipLaunchKernelGGL(k_seg_bounds, dim3((D + 1 + 255) / 256), dim3(256), 0, s,

@@ -72,6 +72,28 @@ __global__ void k_gather_soa(const int32_t* __restrict__ perm,
   }
 }
 
+// 64-bit sort key (distance, total count): inside a distance segment pixels
+// of similar depth sit in the same wave, so the q2qnbinom branches (tail
+// side, series vs continued fraction) diverge less
+__global__ void k_dist_count_keys(const int32_t* __restrict__ dist,
+                                  const int32_t* __restrict__ raw, int64_t n,
+                                  int R, uint64_t* __restrict__ keys) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t tot = 0;
+    for (int r = 0; r < R; ++r) tot += (uint32_t)raw[i * R + r];
+    if (tot > 0xffffffffull) tot = 0xffffffffull;
+    keys[i] = ((uint64_t)(uint32_t)dist[i] << 32) | tot;
+  }
+}
+
+__global__ void k_key_dist(const uint64_t* __restrict__ keys, int64_t n,
+                           int32_t* __restrict__ dist_s) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dist_s[i] = (int32_t)(keys[i] >> 32);
+}
+
 // seg_start[d] = first index with dist_s >= d (d = 0..D)
 __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
                              int D, int64_t* __restrict__ seg_start) {
@@ -93,8 +115,9 @@ __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
 // segment's current dispersion, write pseudodata, then the NLL term at the
 // first Brent point. NLL pass: the NLL term (dispersion.py:67-70) at the
 // segment's current Brent point. Block partial -> partial[w].
-template <int M>
-__global__ __launch_bounds__(kBlock) void k_disp_work(
+// W = minimum waves per SIMD requested from the register allocator
+template <int M, int W = 1>
+__global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int32_t* __restrict__ raw_s, const double* __restrict__ f_s,
     double* __restrict__ pd, int64_t n, const int64_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_len, const int32_t* __restrict__ chunk_d,
@@ -116,7 +139,50 @@ __global__ __launch_bounds__(kBlock) void k_disp_work(
                 (unsigned long long)chunk_len[chunk] * nr);
     double term = 0.0;
     const int i = threadIdx.x;
-    if (i < chunk_len[chunk]) {
+    if (i < chunk_len[chunk] && nr < 8) {
+      // Rolled replicate loop: the q2qnbinom code (the bulk of the kernel)
+      // is emitted once instead of once per replicate slot. Sums run
+      // sequentially from 0 in replicate order = numpy's row sum for n < 8.
+      const int64_t px = chunk_start[chunk] + i;
+      const NllConst kc = st[s].k;
+      const int32_t* ri = rep_idx + c * kMaxReps;
+      double lgsum = 0.0, z = 0.0;
+      if (phase == kEqualize) {
+        const double alpha = st[s].disp;
+        double x[M], f[M], as[M], lf[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const bool on = k < nr;
+          x[k] = on ? (double)raw_s[(int64_t)ri[k] * n + px] : 0.0;
+          f[k] = on ? f_s[(int64_t)ri[k] * n + px] : 1.0;
+          lf[k] = on ? log(f[k]) : 0.0;
+          as[k] = alpha;
+        }
+        int fl = 0;
+        const double f_mean = exp(np_sum<M>(lf, nr) / nr) - 0.0;
+        const double mu = fit_mu<M>(x, f, as, nr, ~0u, &fl);
+        if (fl) atomicOr(&seg_flags[s], fl);
+        double mu_out = mu * f_mean;
+#pragma unroll 1
+        for (int k = 0; k < nr; ++k) {
+          const int64_t o = (int64_t)ri[k] * n + px;
+          double mu_in = mu * f_s[o];
+          const double dk = q2q((double)raw_s[o], &mu_in, &mu_out, alpha);
+          pd[o] = dk;
+          lgsum += lgam(dk + kc.r);
+          z += dk;
+        }
+      } else {
+#pragma unroll 1
+        for (int k = 0; k < nr; ++k) {
+          const double dk = pd[(int64_t)ri[k] * n + px];
+          lgsum += lgam(dk + kc.r);
+          z += dk;
+        }
+      }
+      term = lgsum + kc.lg_nr - lgam(z + kc.nr) - kc.n_lg_r;
+    } else if (M >= 8 && i < chunk_len[chunk]) {
+      // >= 8 replicates in the condition: numpy's pairwise row sums
       const int64_t px = chunk_start[chunk] + i;
       double d[M];
       int ri[M];

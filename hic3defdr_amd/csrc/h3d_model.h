@@ -179,14 +179,34 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
   const double v_in = mi * r_in, v_out = mo * r_out;
   const double sd_in = sqrt(v_in), sd_out = sqrt(v_out);
   const double a_in = mi / r_in, a_out = mo / r_out;
-  double qn, qg;
-  if (x >= mi) {
-    qn = norm_isf(norm_sf(x, mi, sd_in), mo, sd_out);
-    qg = gamma_isf(gamma_sf(x, a_in, r_in), a_out, r_out);
+  // right tail: isf(sf(x)); left tail: ppf(cdf(x)). Both tails go through
+  // the same code with a per-lane tail flag (no divergent duplicate paths).
+  const bool right = x >= mi;
+  // normal: sf(x) = ndtr(-z), cdf(x) = ndtr(z); isf(t) = -ndtri(t) sd + mu,
+  // ppf(t) = ndtri(t) sd + mu (t = 0 / 1 give the +-inf support bounds)
+  const double z = (x - mi) / sd_in;
+  const double tn = ndtr(right ? -z : z);
+  const double qn = (right ? -ndtri(tn) : ndtri(tn)) * sd_out + mo;
+  // gamma(a, scale r): sf = Q(a, x/r), cdf = P(a, x/r); isf / ppf invert the
+  // same tail; x/r <= 0 is the support bound (sf 1, cdf 0)
+  const double xs = x / r_in;
+  double tg;
+  if (xs <= 0.0) {
+    tg = right ? 1.0 : 0.0;
   } else {
-    qn = norm_ppf(norm_cdf(x, mi, sd_in), mo, sd_out);
-    qg = gamma_ppf(gamma_cdf(x, a_in, r_in), a_out, r_out);
+    double P, Q, fac;
+    igam_pq(a_in, xs, lgam(a_in), &P, &Q, &fac);
+    tg = right ? Q : P;
   }
+  double qg;
+  if (tg != tg)
+    qg = NAN;
+  else if (tg == 0.0)
+    qg = right ? INFINITY : 0.0;
+  else if (tg == 1.0)
+    qg = right ? 0.0 : INFINITY;
+  else
+    qg = igam_inv(a_out, tg, right, lgam(a_out)) * r_out;
   double pc = (qn + qg) / 2;
   if (!(pc >= 0.0)) pc = 0.0;
   return pc;

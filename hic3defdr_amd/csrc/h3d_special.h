@@ -157,10 +157,10 @@ H3D_HD double stirling_corr(double a) {
                                             r2 * (1.0 / 156.0)))))));
 }
 
-// x^a e^-x / Gamma(a).
-H3D_HD double igam_fac(double a, double x) {
+// x^a e^-x / Gamma(a), given lga = lgam(a).
+H3D_HD double igam_fac_l(double a, double x, double lga) {
   if (fabs(a - x) > 0.4 * fabs(a) || a < 10.0) {
-    double ax = a * log(x) - x - lgam(a);
+    double ax = a * log(x) - x - lga;
     if (ax < -kMaxLog) return 0.0;
     return exp(ax);
   }
@@ -168,10 +168,10 @@ H3D_HD double igam_fac(double a, double x) {
   return exp(a * log1pmx(s) + 0.5 * log(a / kTwoPi) - stirling_corr(a));
 }
 
-// P(a, x) by its power series (DLMF 8.11.4).
-H3D_HD double igam_series(double a, double x) {
-  double ax = igam_fac(a, x);
-  if (ax == 0.0) return 0.0;
+H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
+
+// power series sum of P(a, x) = fac / a * sum (DLMF 8.11.4)
+H3D_HD double igam_series_sum(double a, double x) {
   double r = a, c = 1.0, ans = 1.0;
   for (int i = 0; i < kMaxIter; ++i) {
     r += 1.0;
@@ -179,11 +179,18 @@ H3D_HD double igam_series(double a, double x) {
     ans += c;
     if (c <= kMachEp * ans) break;
   }
-  return ans * ax / a;
+  return ans;
 }
 
-// Q(a, x) for small x without cancellation (DLMF 8.7.3).
-H3D_HD double igamc_series(double a, double x) {
+// P(a, x) by its power series.
+H3D_HD double igam_series(double a, double x) {
+  double ax = igam_fac(a, x);
+  if (ax == 0.0) return 0.0;
+  return igam_series_sum(a, x) * ax / a;
+}
+
+// Q(a, x) for small x without cancellation (DLMF 8.7.3), given lga.
+H3D_HD double igamc_series_l(double a, double x, double lga) {
   double fac = 1.0, sum = 0.0;
   for (int n = 1; n < kMaxIter; ++n) {
     fac *= -x / n;
@@ -193,13 +200,15 @@ H3D_HD double igamc_series(double a, double x) {
   }
   double logx = log(x);
   double term = -expm1(a * logx - lgam1p(a));
-  return term - exp(a * logx - lgam(a)) * sum;
+  return term - exp(a * logx - lga) * sum;
 }
 
-// Q(a, x) by the continued fraction (DLMF 8.9.2).
-H3D_HD double igamc_cf(double a, double x) {
-  double ax = igam_fac(a, x);
-  if (ax == 0.0) return 0.0;
+H3D_HD double igamc_series(double a, double x) {
+  return igamc_series_l(a, x, lgam(a));
+}
+
+// continued-fraction value of Q(a, x) / fac (DLMF 8.9.2)
+H3D_HD double igamc_cf_ratio(double a, double x) {
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
   double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
   double ans = pkm1 / qkm1;
@@ -230,7 +239,41 @@ H3D_HD double igamc_cf(double a, double x) {
     }
     if (t <= kMachEp) break;
   }
-  return ans * ax;
+  return ans;
+}
+
+// Q(a, x) by the continued fraction.
+H3D_HD double igamc_cf(double a, double x) {
+  double ax = igam_fac(a, x);
+  if (ax == 0.0) return 0.0;
+  return igamc_cf_ratio(a, x) * ax;
+}
+
+// P(a, x), Q(a, x) and fac = x^a e^-x / Gamma(a) in one evaluation, given
+// lga = lgam(a) (a > 0, x > 0 finite). The branch structure follows cephes
+// igam/igamc: the tail that is computed directly is the accurate one, the
+// other is 1 - it.
+H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
+                    double* fac) {
+  const double f = igam_fac_l(a, x, lga);
+  *fac = f;
+  if (x > 1.0 && x > a) {  // continued fraction for the upper tail
+    const double q = (f == 0.0) ? 0.0 : igamc_cf_ratio(a, x) * f;
+    *Q = q;
+    *P = 1.0 - q;
+    return;
+  }
+  const bool small_upper =
+      (x <= 1.1) && ((x <= 0.5) ? !(-0.4 / log(x) < a) : !(x * 1.1 < a));
+  if (small_upper) {  // Q without cancellation when P is close to 1
+    const double q = igamc_series_l(a, x, lga);
+    *Q = q;
+    *P = 1.0 - q;
+    return;
+  }
+  const double p = (f == 0.0) ? 0.0 : igam_series_sum(a, x) * f / a;
+  *P = p;
+  *Q = 1.0 - p;
 }
 
 H3D_HD double igamc(double a, double x);
@@ -309,7 +352,8 @@ H3D_HD double ndtri_lower(double q) {
         t /
         (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1.0);
   }
-  for (int it = 0; it < 2; ++it) {
+  // Acklam's guess is good to 1.2e-9 relative: one Halley step is enough
+  for (int it = 0; it < 1; ++it) {
     // residual Phi(x) - q; near the centre via erf (q - 0.5 exact there)
     double e = (q > 0.25) ? 0.5 * erf(x * kSqrt1_2) - (q - 0.5)
                           : 0.5 * erfc(-x * kSqrt1_2) - q;
@@ -376,13 +420,13 @@ H3D_HD double dm_sn(double a, double x, int N, double tol) {
 }
 
 // DiDonato & Morris (1986) initial guess for the inverse of P(a, .) = p,
-// Q(a, .) = q (p + q = 1).
-H3D_HD double find_inverse_gamma(double a, double p, double q) {
+// Q(a, .) = q (p + q = 1), given lga = lgam(a).
+H3D_HD double find_inverse_gamma(double a, double p, double q, double lga) {
   double result;
   if (a == 1.0) {
     result = (q > 0.9) ? -log1p(-p) : -log(q);
   } else if (a < 1.0) {
-    double g = exp(lgam(a));
+    double g = exp(lga);
     double b = q * g;
     if ((b > 0.6) || ((b >= 0.45) && (a >= 0.3))) {
       double u;
@@ -423,8 +467,7 @@ H3D_HD double find_inverse_gamma(double a, double p, double q) {
         result = w;
       } else {
         double D = fmax(2.0, a * (a - 1));
-        double lg = lgam(a);
-        double lb = log(q) + lg;
+        double lb = log(q) + lga;
         if (lb < -D * 2.3) {
           result = dm_eq25(a, -lb);
         } else {
@@ -435,8 +478,9 @@ H3D_HD double find_inverse_gamma(double a, double p, double q) {
     } else {
       double z = w;
       double ap1 = a + 1, ap2 = a + 2;
+      const double lg_ap1 = lga + log(a);  // lgam(a + 1)
       if (w < 0.15 * ap1) {
-        double v = log(p) + lgam(ap1);
+        double v = log(p) + lg_ap1;
         z = exp((v + w) / a);
         s = log1p(z / ap1 * (1 + z / ap2));
         z = exp((v + z - s) / a);
@@ -449,7 +493,7 @@ H3D_HD double find_inverse_gamma(double a, double p, double q) {
         result = z;
       } else {
         double ls = log(dm_sn(a, z, 100, 1e-4));
-        double v = log(p) + lgam(ap1);
+        double v = log(p) + lg_ap1;
         z = exp((v + z - ls) / a);
         result = z * (1 - (a * log(z) - z - v + ls) / (a - z));
       }
@@ -458,26 +502,34 @@ H3D_HD double find_inverse_gamma(double a, double p, double q) {
   return result;
 }
 
-// Halley refinement shared by igami/igamci. upper=false solves P(a,x)=p,
-// upper=true solves Q(a,x)=q. Three steps as scipy, continued (up to 8) only
-// while the last step still moved x by more than 1e-12 relative.
-H3D_HD double igam_halley(double a, double x, double target, bool upper) {
+// Inverse incomplete gamma on either tail: solves P(a, x) = t (upper=false)
+// or Q(a, x) = t (upper=true), t in (0, 1), given lga = lgam(a). As scipy's
+// igami/igamci it always works on the tail that is <= 0.9 and refines the
+// DiDonato & Morris guess with Halley steps (f''/f' = (a-1)/x - 1); each step
+// costs one igam_pq. It stops once a step moved x by <= 1e-6 relative: Halley
+// converges cubically, so the error left is ~1e-18 (scipy always takes 3).
+H3D_HD double igam_inv(double a, double t, bool upper, double lga) {
+  if (t > 0.9) {
+    t = 1.0 - t;
+    upper = !upper;
+  }
+  double x = upper ? find_inverse_gamma(a, 1.0 - t, t, lga)
+                   : find_inverse_gamma(a, t, 1.0 - t, lga);
   for (int i = 0; i < 8; ++i) {
-    double fac = igam_fac(a, x);
+    double P, Q, fac;
+    igam_pq(a, x, lga, &P, &Q, &fac);
     if (fac == 0.0) return x;
-    double f_fp = upper ? (igamc(a, x) - target) * x / (-fac)
-                        : (igam(a, x) - target) * x / fac;
-    double fpp_fp = -1.0 + (a - 1) / x;
-    double xn = is_inf(fpp_fp) ? x - f_fp : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
+    const double f_fp = upper ? (Q - t) * x / (-fac) : (P - t) * x / fac;
+    const double fpp_fp = -1.0 + (a - 1) / x;
+    double xn = is_inf(fpp_fp) ? x - f_fp
+                               : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
     if (!(xn > 0.0)) xn = 0.5 * x;  // safeguard: stay in the support
-    double dx = fabs(xn - x);
+    const double dx = fabs(xn - x);
     x = xn;
-    if (i >= 2 && dx <= 1e-12 * x) break;
+    if (dx <= 1e-6 * x) break;
   }
   return x;
 }
-
-H3D_HD double igamci(double a, double q);
 
 // Inverse of P(a, .) (scipy gammaincinv).
 H3D_HD double igami(double a, double p) {
@@ -485,9 +537,7 @@ H3D_HD double igami(double a, double p) {
   if (a < 0.0 || p < 0.0 || p > 1.0) return NAN;
   if (p == 0.0) return 0.0;
   if (p == 1.0) return INFINITY;
-  if (p > 0.9) return igamci(a, 1.0 - p);
-  double x = find_inverse_gamma(a, p, 1.0 - p);
-  return igam_halley(a, x, p, false);
+  return igam_inv(a, p, false, lgam(a));
 }
 
 // Inverse of Q(a, .) (scipy gammainccinv).
@@ -496,9 +546,7 @@ H3D_HD double igamci(double a, double q) {
   if (a < 0.0 || q < 0.0 || q > 1.0) return NAN;
   if (q == 0.0) return INFINITY;
   if (q == 1.0) return 0.0;
-  if (q > 0.9) return igami(a, 1.0 - q);
-  double x = find_inverse_gamma(a, 1.0 - q, q);
-  return igam_halley(a, x, q, true);
+  return igam_inv(a, q, true, lgam(a));
 }
 
 // chi2(df).sf(x) as scipy.stats: support lower bound -> 1 (cephes chdtrc).
