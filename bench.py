@@ -175,6 +175,7 @@ def main():
         l_ms, l_n, l_px = ctx.profile_read('lrt')
         r_ms, r_n, _ = ctx.profile_read('disp_reduce')
         u_ms, u_n, _ = ctx.profile_read('disp_update')
+        n_ms, n_n, _ = ctx.profile_read('disp_nll')
         p_ms, p_n, _ = ctx.profile_read('disp_prep')
         tot_px = n
         if dist:
@@ -221,6 +222,7 @@ def main():
                     'disp_work': w_ms / args.steps,
                     'disp_reduce': r_ms / args.steps,
                     'disp_update': u_ms / args.steps,
+                    'disp_nll': n_ms / args.steps,
                     'disp_prep': p_ms / args.steps,
                     'lrt': l_ms / args.steps},
                 'lrt_roofline': {'achieved': l_ach, 'peak': peak,

@@ -166,30 +166,40 @@ void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
                       const int64_t* cs, const int32_t* cl, const int32_t* cd,
                       int C, const int32_t* rep_idx, const int32_t* n_rep,
                       const SegState* st, int* seg_flags, const int32_t* list,
-                      const int32_t* list_len, double* partial) {
-  if (M == 4 && ctx->disp_w == 4)
-    hipLaunchKernelGGL((k_disp_work<M, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
-                       seg_flags, list, list_len, partial, ctx->work_count);
-  else if (M == 4 && ctx->disp_w == 3)
-    hipLaunchKernelGGL((k_disp_work<M, 3>), dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
-                       seg_flags, list, list_len, partial, ctx->work_count);
-  else
-    hipLaunchKernelGGL((k_disp_work<M, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, st,
-                       seg_flags, list, list_len, partial, ctx->work_count);
+                      const int32_t* meta, double* partial) {
+  // equalize pass (heavy: q2qnbinom), then the NLL-only pass (light)
+  {
+    ProfScope ps(ctx, "disp_work", 0);
+    if (M == 4 && ctx->disp_w == 4)
+      hipLaunchKernelGGL((k_disp_work<M, 4, kEqualize>), dim3(grid), dim3(kBlock), 0,
+                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
+                         st, seg_flags, list, meta, partial, ctx->work_count);
+    else if (M == 4 && ctx->disp_w == 3)
+      hipLaunchKernelGGL((k_disp_work<M, 3, kEqualize>), dim3(grid), dim3(kBlock), 0,
+                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
+                         st, seg_flags, list, meta, partial, ctx->work_count);
+    else
+      hipLaunchKernelGGL((k_disp_work<M, 1, kEqualize>), dim3(grid), dim3(kBlock), 0,
+                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
+                         st, seg_flags, list, meta, partial, ctx->work_count);
+  }
+  {
+    ProfScope ps(ctx, "disp_nll", 0);
+    hipLaunchKernelGGL((k_disp_work<M, 1, kNll>), dim3(grid), dim3(kBlock), 0,
+                       ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
+                       st, seg_flags, list, meta, partial, ctx->work_count);
+  }
 }
 
 // algorithmic HBM bytes of the disp_work launches so far: an equalize
 // pixel-replicate reads raw (4 B) + f (8 B) and writes pseudodata (8 B); an
 // NLL pixel-replicate reads pseudodata (8 B)
-int64_t disp_work_bytes(h3d_ctx* ctx) {
+int64_t disp_work_bytes(h3d_ctx* ctx, bool nll) {
   unsigned long long c[2] = {0, 0};
   if (!ctx->work_count) return 0;
   (void)hipMemcpyAsync(c, ctx->work_count, sizeof(c), hipMemcpyDeviceToHost, ctx->stream);
   (void)hipStreamSynchronize(ctx->stream);
-  return (int64_t)(c[0] * 20ull + c[1] * 8ull);
+  return nll ? (int64_t)(c[1] * 8ull) : (int64_t)(c[0] * 20ull);
 }
 
 template <int M, int CM>
@@ -312,8 +322,11 @@ int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
   ProfEntry e = (it == ctx->stats.end()) ? ProfEntry() : it->second;
   if (total_ms) *total_ms = e.ms;
   if (launches) *launches = e.launches;
-  // disp_work units = algorithmic bytes; lrt / disp_prep units = pixels
-  if (units) *units = std::strcmp(name, "disp_work") == 0 ? disp_work_bytes(ctx) : e.units;
+  // disp_work / disp_nll units = algorithmic bytes; lrt / disp_prep = pixels
+  if (units)
+    *units = std::strcmp(name, "disp_work") == 0   ? disp_work_bytes(ctx, false)
+             : std::strcmp(name, "disp_nll") == 0 ? disp_work_bytes(ctx, true)
+                                                   : e.units;
   return 0;
 }
 
@@ -442,7 +455,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   SegState* d_st = (SegState*)up("seg_state", st.data(), S * sizeof(SegState));
   const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
   int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
-  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // list_len, active
+  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len
   int32_t* d_slb = (int32_t*)scratch(ctx, "seg_lb", S * 4);
   int32_t* d_sle = (int32_t*)scratch(ctx, "seg_le", S * 4);
   double* d_partial = (double*)scratch(ctx, "partial", max_items * 8);
@@ -457,8 +470,8 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 
   // initial active list
   hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
-                     d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_meta, d_slb,
-                     d_sle, d_res, d_meta + 1, 1);
+                     d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
+                     d_res, d_meta, 1);
   const int work_grid = std::max(1, std::min<int>((int)max_items, ctx->n_cu * 4));
   int32_t* h_meta = nullptr;
   HIP_TRY(hipHostMalloc((void**)&h_meta, 16, hipHostMallocDefault));
@@ -466,7 +479,6 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   while (true) {
     for (int b = 0; b < batch; ++b) {
       {
-        ProfScope ps(ctx, "disp_work", 0);
         switch (maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32) {
           case 4:
             launch_disp_work<4>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
@@ -493,8 +505,8 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       {
         ProfScope ps(ctx, "disp_update", 0);
         hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
-                           d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_meta,
-                           d_slb, d_sle, d_res, d_meta + 1, 0);
+                           d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb,
+                           d_sle, d_res, d_meta, 0);
       }
       ++rounds;
     }

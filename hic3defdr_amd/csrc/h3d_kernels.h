@@ -115,8 +115,11 @@ __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
 // segment's current dispersion, write pseudodata, then the NLL term at the
 // first Brent point. NLL pass: the NLL term (dispersion.py:67-70) at the
 // segment's current Brent point. Block partial -> partial[w].
-// W = minimum waves per SIMD requested from the register allocator
-template <int M, int W = 1>
+// PH = the pass this instantiation runs (kEqualize or kNll): the list holds
+// the equalize items first (meta[2] of them), then the NLL items, and each
+// pass is its own kernel so the light NLL pass is not held to the register
+// budget of q2qnbinom. W = minimum waves per SIMD asked of the allocator.
+template <int M, int W, int PH>
 __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int32_t* __restrict__ raw_s, const double* __restrict__ f_s,
     double* __restrict__ pd, int64_t n, const int64_t* __restrict__ chunk_start,
@@ -124,15 +127,17 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     int C, const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
     const int32_t* __restrict__ n_rep /* C */, const SegState* __restrict__ st,
     int* __restrict__ seg_flags, const int32_t* __restrict__ list,
-    const int32_t* __restrict__ list_len, double* __restrict__ partial,
+    const int32_t* __restrict__ meta /* [len, active, eq_len] */,
+    double* __restrict__ partial,
     unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
   __shared__ double lds[kBlock / 64];
-  const int len = *list_len;
-  for (int w = blockIdx.x; w < len; w += gridDim.x) {
+  const int beg = (PH == kEqualize) ? 0 : meta[2];
+  const int end = (PH == kEqualize) ? meta[2] : meta[0];
+  for (int w = beg + blockIdx.x; w < end; w += gridDim.x) {
     const int item = list[w];
     const int chunk = item / C, c = item - chunk * C;
     const int s = chunk_d[chunk] * C + c;
-    const int phase = st[s].phase;
+    constexpr int phase = PH;
     const int nr = n_rep[c];
     if (threadIdx.x == 0)
       atomicAdd(&work_count[phase == kEqualize ? 0 : 1],
@@ -163,11 +168,12 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
         const double mu = fit_mu<M>(x, f, as, nr, ~0u, &fl);
         if (fl) atomicOr(&seg_flags[s], fl);
         double mu_out = mu * f_mean;
+        LgamCache cache;
 #pragma unroll 1
         for (int k = 0; k < nr; ++k) {
           const int64_t o = (int64_t)ri[k] * n + px;
           double mu_in = mu * f_s[o];
-          const double dk = q2q((double)raw_s[o], &mu_in, &mu_out, alpha);
+          const double dk = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
           pd[o] = dk;
           lgsum += lgam(dk + kc.r);
           z += dk;
@@ -243,30 +249,32 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     const int* __restrict__ seg_flags, int S, int C,
     const int32_t* __restrict__ n_rep, const int32_t* __restrict__ seg_chunk_b,
     const int32_t* __restrict__ seg_chunk_e, int32_t* __restrict__ list,
-    int32_t* __restrict__ list_len, int32_t* __restrict__ seg_lb,
+    int32_t* __restrict__ seg_lb,
     int32_t* __restrict__ seg_le, double* __restrict__ result,
-    int32_t* __restrict__ active, int first) {
+    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first) {
   __shared__ int32_t scan[1024];
   __shared__ int32_t base_s;
   if (threadIdx.x == 0) base_s = 0;
   __syncthreads();
+  // advance the state machines
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    SegState cur = st[s];
+    if (!first && cur.phase != kDone) {
+      cur.flags |= seg_flags[s];
+      seg_step(&cur, seg_total[s], n_rep[s % C]);
+      st[s] = cur;
+    }
+    if (cur.phase == kDone) result[s] = cur.result;
+  }
+  __syncthreads();
+  // list: equalize items of every segment first, then the NLL items
+  for (int pass = 0; pass < 2; ++pass) {
+  const int want = pass == 0 ? kEqualize : kNll;
   for (int s0 = 0; s0 < S; s0 += blockDim.x) {
     const int s = s0 + threadIdx.x;
     int cnt = 0;
-    if (s < S) {
-      SegState cur = st[s];
-      const int c = s % C;
-      if (!first && cur.phase != kDone) {
-        cur.flags |= seg_flags[s];
-        seg_step(&cur, seg_total[s], n_rep[c]);
-        st[s] = cur;
-      }
-      if (cur.phase == kDone) {
-        result[s] = cur.result;
-      } else {
-        cnt = seg_chunk_e[s / C] - seg_chunk_b[s / C];
-      }
-    }
+    if (s < S && st[s].phase == want)
+      cnt = seg_chunk_e[s / C] - seg_chunk_b[s / C];
     scan[threadIdx.x] = cnt;
     __syncthreads();
     for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // inclusive scan
@@ -277,7 +285,7 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     }
     const int base = base_s;
     const int beg = base + scan[threadIdx.x] - cnt;
-    if (s < S) {
+    if (s < S && (cnt > 0 || pass == 0)) {
       seg_lb[s] = beg;
       seg_le[s] = beg + cnt;
       const int d = s / C, c = s % C;
@@ -288,9 +296,11 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     if (threadIdx.x == blockDim.x - 1) base_s = base + scan[threadIdx.x];
     __syncthreads();
   }
+  if (pass == 0 && threadIdx.x == 0) meta[2] = base_s;
+  }
   if (threadIdx.x == 0) {
-    *list_len = base_s;
-    *active = base_s;
+    meta[0] = base_s;
+    meta[1] = base_s;
   }
 }
 

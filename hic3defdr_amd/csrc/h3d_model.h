@@ -169,7 +169,23 @@ H3D_HD double gamma_ppf(double q, double shape, double scale) {
 // q2qnbinom for one value (scaled_nb.py:217-275). mu_in / mu_out are
 // clamped IN PLACE exactly as the reference does (:240-242) so the caller can
 // carry the mu_out clamp into the next replicate (equalize, :209-213).
-H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
+// lgamma of the output shape, reused across the replicates of a pixel (they
+// share mu_out unless a clamp changes it)
+struct LgamCache {
+  double a = -1.0, lga = 0.0;
+};
+
+H3D_HD double lgam_cached(double a, LgamCache* c) {
+  if (!c) return lgam(a);
+  if (a != c->a) {
+    c->a = a;
+    c->lga = lgam(a);
+  }
+  return c->lga;
+}
+
+H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha,
+                  LgamCache* cache = nullptr) {
   if (!((*mu_in >= 0.25) && (*mu_out >= 0.25))) {
     *mu_in = 0.25;
     *mu_out = 0.25;
@@ -182,11 +198,22 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
   // right tail: isf(sf(x)); left tail: ppf(cdf(x)). Both tails go through
   // the same code with a per-lane tail flag (no divergent duplicate paths).
   const bool right = x >= mi;
-  // normal: sf(x) = ndtr(-z), cdf(x) = ndtr(z); isf(t) = -ndtri(t) sd + mu,
-  // ppf(t) = ndtri(t) sd + mu (t = 0 / 1 give the +-inf support bounds)
+  // normal: isf(sf(x)) = ppf(cdf(x)) = mo + sd_out (x - mi) / sd_in exactly;
+  // the reference's ndtr/ndtri round trip only adds rounding (<= 1e-16 of
+  // the result) -- except where its ndtr underflows to 0 (|z| > 37.68), and
+  // then isf(0) / ppf(0) are the +-inf support bounds
   const double z = (x - mi) / sd_in;
-  const double tn = ndtr(right ? -z : z);
-  const double qn = (right ? -ndtri(tn) : ndtri(tn)) * sd_out + mo;
+  const double zh = z * kSqrt1_2;  // the erfc argument of ndtr
+  const bool under = zh * zh > kMaxLog;
+  double qn;
+  if (z != z)
+    qn = NAN;
+  else if (right && z > 0.0 && under)
+    qn = INFINITY;
+  else if (!right && z < 0.0 && under)
+    qn = -INFINITY;
+  else
+    qn = z * sd_out + mo;
   // gamma(a, scale r): sf = Q(a, x/r), cdf = P(a, x/r); isf / ppf invert the
   // same tail; x/r <= 0 is the support bound (sf 1, cdf 0)
   const double xs = x / r_in;
@@ -199,14 +226,27 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha) {
     tg = right ? Q : P;
   }
   double qg;
-  if (tg != tg)
+  if (tg != tg) {
     qg = NAN;
-  else if (tg == 0.0)
+  } else if (tg == 0.0) {
     qg = right ? INFINITY : 0.0;
-  else if (tg == 1.0)
+  } else if (tg == 1.0) {
     qg = right ? 0.0 : INFINITY;
-  else
-    qg = igam_inv(a_out, tg, right, lgam(a_out)) * r_out;
+  } else {
+    // initial guess: carry x through the Wilson-Hilferty cube-root normal
+    // approximation of gamma(a_in) into gamma(a_out) -- the approximation
+    // errors of the two shapes largely cancel, so Halley usually needs one
+    // step; DiDonato-Morris below shape 1, where Wilson-Hilferty is poor
+    double guess = -1.0;
+    if (a_in >= 1.0 && a_out >= 1.0) {
+      const double m_in = 1.0 - 1.0 / (9.0 * a_in);
+      const double m_out = 1.0 - 1.0 / (9.0 * a_out);
+      const double zz = (cbrt(xs / a_in) - m_in) * sqrt(9.0 * a_in);
+      const double y = m_out + zz / sqrt(9.0 * a_out);
+      if (y > 0.0) guess = a_out * y * y * y;
+    }
+    qg = igam_inv(a_out, tg, right, lgam_cached(a_out, cache), guess) * r_out;
+  }
   double pc = (qn + qg) / 2;
   if (!(pc >= 0.0)) pc = 0.0;
   return pc;
@@ -228,11 +268,12 @@ H3D_HD int equalize_pixel(const double* x, const double* f, int n, double alpha,
   int st = 0;
   const double mu = fit_mu<M>(x, f, as, n, ~0u, &st);
   double mu_out = mu * f_mean;
+  LgamCache cache;
 #pragma unroll
   for (int k = 0; k < M; ++k)
     if (k < n) {
       double mu_in = mu * f[k];
-      out[k] = q2q(x[k], &mu_in, &mu_out, alpha);
+      out[k] = q2q(x[k], &mu_in, &mu_out, alpha, &cache);
     }
   return st;
 }

@@ -508,13 +508,15 @@ H3D_HD double find_inverse_gamma(double a, double p, double q, double lga) {
 // DiDonato & Morris guess with Halley steps (f''/f' = (a-1)/x - 1); each step
 // costs one igam_pq. It stops once a step moved x by <= 1e-6 relative: Halley
 // converges cubically, so the error left is ~1e-18 (scipy always takes 3).
-H3D_HD double igam_inv(double a, double t, bool upper, double lga) {
+H3D_HD double igam_inv(double a, double t, bool upper, double lga,
+                       double guess = -1.0) {
   if (t > 0.9) {
     t = 1.0 - t;
     upper = !upper;
   }
-  double x = upper ? find_inverse_gamma(a, 1.0 - t, t, lga)
-                   : find_inverse_gamma(a, t, 1.0 - t, lga);
+  double x = (guess > 0.0) ? guess
+                           : upper ? find_inverse_gamma(a, 1.0 - t, t, lga)
+                                   : find_inverse_gamma(a, t, 1.0 - t, lga);
   for (int i = 0; i < 8; ++i) {
     double P, Q, fac;
     igam_pq(a, x, lga, &P, &Q, &fac);

@@ -141,10 +141,11 @@ int h3d_bh(const double* p, int64_t n, double* q);
 
 /* ---- measurement -------------------------------------------------------- */
 
-/* Per-kernel HIP-event timing on the ctx stream. name in {"disp_work",
- * "disp_reduce", "disp_update", "disp_prep", "lrt"}. units: algorithmic
- * HBM bytes for "disp_work" (counted on the device since the last reset),
- * pixels for "lrt" / "disp_prep". */
+/* Per-kernel HIP-event timing on the ctx stream. name in {"disp_work" (the
+ * equalize pass), "disp_nll", "disp_reduce", "disp_update", "disp_prep",
+ * "lrt"}. units: algorithmic HBM bytes for "disp_work" / "disp_nll"
+ * (counted on the device since the last reset), pixels for "lrt" /
+ * "disp_prep". */
 int h3d_profile_enable(h3d_ctx* ctx, int on);
 int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
                      int64_t* launches, int64_t* units);
