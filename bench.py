@@ -175,7 +175,7 @@ def main():
         l_ms, l_n, l_px = ctx.profile_read('lrt')
         r_ms, r_n, _ = ctx.profile_read('disp_reduce')
         u_ms, u_n, _ = ctx.profile_read('disp_update')
-        n_ms, n_n, _ = ctx.profile_read('disp_nll')
+        n_ms, n_n, n_bytes = ctx.profile_read('disp_nll')
         p_ms, p_n, _ = ctx.profile_read('disp_prep')
         tot_px = n
         if dist:
@@ -217,7 +217,8 @@ def main():
                     'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
                     'note': 'FP64-VALU/transcendental bound (SURVEY.md '
                             'finding 3); bytes = 20 B per equalize '
-                            'pixel-replicate + 8 B per NLL pixel-replicate'},
+                            'pixel-replicate (raw 4 + f 8 in, pseudodata 8 '
+                            'out)'},
                 'kernels_ms_per_step': {
                     'disp_work': w_ms / args.steps,
                     'disp_reduce': r_ms / args.steps,
@@ -225,6 +226,17 @@ def main():
                     'disp_nll': n_ms / args.steps,
                     'disp_prep': p_ms / args.steps,
                     'lrt': l_ms / args.steps},
+                'work_per_step': {
+                    'equalize_pixel_reps': w_bytes / 20.0 / args.steps,
+                    'nll_pixel_reps': n_bytes / 8.0 / args.steps,
+                    'disp_launches': w_n / args.steps},
+                'nll_roofline': {
+                    'achieved': n_bytes / (n_ms / 1e3) / 1e9 if n_ms else 0.0,
+                    'peak': peak, 'unit': 'GB/s',
+                    'frac': n_bytes / (n_ms / 1e3) / 1e9 / peak if n_ms
+                    else 0.0,
+                    'bytes_per_pixel_rep': 8,
+                    'avg_launch_us': n_ms / max(n_n, 1) * 1e3},
                 'lrt_roofline': {'achieved': l_ach, 'peak': peak,
                                  'unit': 'GB/s', 'frac': l_ach / peak,
                                  'bytes_per_pixel': bytes_per_lrt_pixel(R, C),

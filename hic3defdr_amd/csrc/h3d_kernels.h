@@ -167,14 +167,48 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
         const double f_mean = exp(np_sum<M>(lf, nr) / nr) - 0.0;
         const double mu = fit_mu<M>(x, f, as, nr, ~0u, &fl);
         if (fl) atomicOr(&seg_flags[s], fl);
-        double mu_out = mu * f_mean;
+        const double mu_out0 = mu * f_mean;
+        // The reference clamps (mu_in, mu_out) to 0.25 in place and carries
+        // the clamped mu_out into the later replicates (scaled_nb.py:209-213,
+        // 240-242). Resolve that carry first -- fc = the first replicate
+        // whose pair fails the >= 0.25 test -- so the replicates can be
+        // visited in any order: upper-tail ones (x >= mu_in: the continued
+        // fraction path of the incomplete gamma) first, then lower-tail ones
+        // (power series). Lanes of a wave then run the same branch of
+        // igam_pq in each slot instead of serialising both.
+        int fc = nr;
+        unsigned up = 0u, lo = 0u;
+#pragma unroll
+        for (int k = M - 1; k >= 0; --k)
+          if (k < nr) {
+            const double mi = mu * f[k];
+            if (!(mi >= 0.25 && mu_out0 >= 0.25)) fc = k;
+            if (x[k] >= mi)
+              up |= 1u << k;
+            else
+              lo |= 1u << k;
+          }
         LgamCache cache;
 #pragma unroll 1
-        for (int k = 0; k < nr; ++k) {
+        for (int j = 0; j < nr; ++j) {
+          int k;
+          if (up) {
+            k = __builtin_ctz(up);
+            up &= up - 1u;
+          } else {
+            k = __builtin_ctz(lo);
+            lo &= lo - 1u;
+          }
           const int64_t o = (int64_t)ri[k] * n + px;
           double mu_in = mu * f_s[o];
-          const double dk = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
-          pd[o] = dk;
+          double mu_out = (k > fc) ? 0.25 : mu_out0;
+          pd[o] = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
+        }
+        // NLL term in replicate order (numpy's row sum), from the values
+        // this thread just wrote
+#pragma unroll 1
+        for (int k = 0; k < nr; ++k) {
+          const double dk = pd[(int64_t)ri[k] * n + px];
           lgsum += lgam(dk + kc.r);
           z += dk;
         }

@@ -84,9 +84,11 @@ H3D_HD double fit_mu(const double* x, const double* b, const double* a, int n,
     *status |= kFlagNoRoot;
     return NAN;
   }
+  H3D_STAT(fit, 1);
   double th = log(init / cnt);
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
+    H3D_STAT(fit_it, 1);
     const double mu = exp(th);
     double g = 0.0, gp = 0.0;
 #pragma unroll
@@ -103,7 +105,13 @@ H3D_HD double fit_mu(const double* x, const double* b, const double* a, int n,
       hi = th;
     else
       return mu;
-    double tn = th - g / gp;
+    const double dn = g / gp;
+    // Newton converges quadratically here (g is smooth and monotone in
+    // theta): once a step is <= 1e-8 the error after it is ~1e-16, so take
+    // it and stop. (Without this exit, a final step below one ulp left th
+    // on the bracket edge and fell through to ~50 bisections.)
+    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp(th - dn);
+    double tn = th - dn;
     if (!(tn > lo && tn < hi)) {
       if (is_inf(lo))
         tn = hi - 2.0;

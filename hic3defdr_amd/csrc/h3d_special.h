@@ -25,6 +25,24 @@
 #define H3D_HD inline
 #endif
 
+// Work counters for tools/q2q_stats (host builds with H3D_INSTRUMENT only;
+// compiled out everywhere else).
+#if defined(H3D_INSTRUMENT) && !defined(__HIP_DEVICE_COMPILE__)
+namespace h3d {
+struct Stats {
+  long pq, cf, su, ser, cf_it, su_it, ser_it, fac_l1, l1_it, inv, halley, wh,
+      lgam, lgam_small, lgam_it, fit, fit_it;
+};
+inline thread_local Stats* g_stats = nullptr;
+}  // namespace h3d
+#define H3D_STAT(field, v) \
+  do {                     \
+    if (h3d::g_stats) h3d::g_stats->field += (v); \
+  } while (0)
+#else
+#define H3D_STAT(field, v) ((void)0)
+#endif
+
 namespace h3d {
 
 constexpr double kMachEp = 1.11022302462515654042e-16;  // 2^-53
@@ -63,15 +81,19 @@ H3D_HD double lgam(double x) {
   const double C[] = {-3.51815701436523470549E2, -1.70642106651881159223E4,
                       -2.20528590553854454839E5, -1.13933444367982507207E6,
                       -2.53252307177582951285E6, -2.01889141433532773231E6};
+  H3D_STAT(lgam, 1);
   if (!(x > 0.0)) return (x == 0.0) ? INFINITY : NAN;
   if (x < 13.0) {
+    H3D_STAT(lgam_small, 1);
     double z = 1.0, p = 0.0, u = x;
     while (u >= 3.0) {
+      H3D_STAT(lgam_it, 1);
       p -= 1.0;
       u = x + p;
       z *= u;
     }
     while (u < 2.0) {
+      H3D_STAT(lgam_it, 1);
       z /= u;
       p += 1.0;
       u = x + p;
@@ -95,17 +117,21 @@ H3D_HD double lgam(double x) {
   return q;
 }
 
-// log(1 + x) - x (cephes log1pmx).
+// log(1 + x) - x (cephes log1pmx). For |x| < 0.5 cephes sums the Taylor
+// series until it converges (up to ~50 terms, a data-dependent loop that
+// diverges across a wave); here it is the fixed-length atanh form
+//   log1p(x) - x = -x^2 / (2 + x) + 2 u^3 sum_k u^2k / (2k + 3),
+//   u = x / (2 + x), |u| <= 1/3,
+// whose 16 terms reach the same ~1 ulp accuracy (the sum is <= 1/12 of the
+// leading term and its truncation error < 9^-16).
 H3D_HD double log1pmx(double x) {
   if (fabs(x) < 0.5) {
-    double xfac = x, res = 0.0;
-    for (int n = 2; n < kMaxIter; ++n) {
-      xfac *= -x;
-      double term = xfac / n;
-      res += term;
-      if (fabs(term) < kMachEp * fabs(res)) break;
-    }
-    return res;
+    H3D_STAT(l1_it, 1);
+    const double u = x / (2.0 + x), v = u * u;
+    double s = 1.0 / 33.0;
+#pragma unroll
+    for (int k = 14; k >= 0; --k) s = s * v + 1.0 / (2 * k + 3);
+    return 2.0 * u * v * s - x * x / (2.0 + x);
   }
   return log1p(x) - x;
 }
@@ -164,6 +190,7 @@ H3D_HD double igam_fac_l(double a, double x, double lga) {
     if (ax < -kMaxLog) return 0.0;
     return exp(ax);
   }
+  H3D_STAT(fac_l1, 1);
   double s = (x - a) / a;
   return exp(a * log1pmx(s) + 0.5 * log(a / kTwoPi) - stirling_corr(a));
 }
@@ -174,6 +201,7 @@ H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
 H3D_HD double igam_series_sum(double a, double x) {
   double r = a, c = 1.0, ans = 1.0;
   for (int i = 0; i < kMaxIter; ++i) {
+    H3D_STAT(ser_it, 1);
     r += 1.0;
     c *= x / r;
     ans += c;
@@ -193,6 +221,7 @@ H3D_HD double igam_series(double a, double x) {
 H3D_HD double igamc_series_l(double a, double x, double lga) {
   double fac = 1.0, sum = 0.0;
   for (int n = 1; n < kMaxIter; ++n) {
+    H3D_STAT(su_it, 1);
     fac *= -x / n;
     double term = fac / (a + n);
     sum += term;
@@ -213,6 +242,7 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
   double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
   double ans = pkm1 / qkm1;
   for (int i = 0; i < kMaxIter; ++i) {
+    H3D_STAT(cf_it, 1);
     c += 1.0;
     y += 1.0;
     z += 2.0;
@@ -255,9 +285,11 @@ H3D_HD double igamc_cf(double a, double x) {
 // other is 1 - it.
 H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
                     double* fac) {
+  H3D_STAT(pq, 1);
   const double f = igam_fac_l(a, x, lga);
   *fac = f;
   if (x > 1.0 && x > a) {  // continued fraction for the upper tail
+    H3D_STAT(cf, 1);
     const double q = (f == 0.0) ? 0.0 : igamc_cf_ratio(a, x) * f;
     *Q = q;
     *P = 1.0 - q;
@@ -266,11 +298,13 @@ H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
   const bool small_upper =
       (x <= 1.1) && ((x <= 0.5) ? !(-0.4 / log(x) < a) : !(x * 1.1 < a));
   if (small_upper) {  // Q without cancellation when P is close to 1
+    H3D_STAT(su, 1);
     const double q = igamc_series_l(a, x, lga);
     *Q = q;
     *P = 1.0 - q;
     return;
   }
+  H3D_STAT(ser, 1);
   const double p = (f == 0.0) ? 0.0 : igam_series_sum(a, x) * f / a;
   *P = p;
   *Q = 1.0 - p;
@@ -510,6 +544,8 @@ H3D_HD double find_inverse_gamma(double a, double p, double q, double lga) {
 // converges cubically, so the error left is ~1e-18 (scipy always takes 3).
 H3D_HD double igam_inv(double a, double t, bool upper, double lga,
                        double guess = -1.0) {
+  H3D_STAT(inv, 1);
+  H3D_STAT(wh, guess > 0.0);
   if (t > 0.9) {
     t = 1.0 - t;
     upper = !upper;
@@ -518,6 +554,7 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
                            : upper ? find_inverse_gamma(a, 1.0 - t, t, lga)
                                    : find_inverse_gamma(a, t, 1.0 - t, lga);
   for (int i = 0; i < 8; ++i) {
+    H3D_STAT(halley, 1);
     double P, Q, fac;
     igam_pq(a, x, lga, &P, &Q, &fac);
     if (fac == 0.0) return x;

@@ -176,3 +176,19 @@ def test_lrt_vs_oracle_r9c3(lib):
     assert st == 0
     assert rel_err(p, rp) < 1e-7
     assert rel_err(m1, rm1) < 1e-9
+
+
+def test_log1pmx_fixed_length_form(lib):
+    # the atanh form replaces cephes' convergent Taylor loop on |x| < 0.5;
+    # reference: log1p(x) - x in extended precision via the series itself
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-0.4999, 0.4999, 20000),
+                        10 ** rng.uniform(-12, -0.31, 5000),
+                        -(10 ** rng.uniform(-12, -0.31, 5000))])
+    ref = np.array([float(sum((-1) ** (n + 1) * np.longdouble(v) ** n / n
+                              for n in range(2, 200)))
+                    for v in x[:3000]])
+    got = unary(lib, 'log1pmx', x)
+    assert rel_err(got[:3000], ref) < 4e-16 * 8
+    big = np.abs(x) > 1e-3  # where log1p(x) - x itself is still accurate
+    assert rel_err(got[big], np.log1p(x[big]) - x[big]) < 1e-10

@@ -1,0 +1,134 @@
+"""Work census of the equalize pass on a cfg2-shaped sample (CPU only).
+
+Builds tools/q2q_stats.cpp with g++, makes a synthetic chromosome with the
+bench generator, estimates dispersions with the oracle, then runs the
+instrumented equalize at the final per-distance dispersion, in the GPU's
+(dist, count) pixel order, and reports per pixel-replicate work and a
+64-lane wave divergence estimate (sum of per-wave max / sum of mean).
+
+    python tools/q2q_stats.py [--bins 1500] [--dmax 250]
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def build():
+    out = os.path.join(tempfile.gettempdir(), 'libq2qstats.so')
+    src = os.path.join(HERE, 'q2q_stats.cpp')
+    subprocess.check_call(['g++', '-O2', '-std=c++17', '-shared', '-fPIC',
+                           '-ffp-contract=off', src, '-o', out])
+    return ctypes.CDLL(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--bins', type=int, default=1500)
+    ap.add_argument('--dmax', type=int, default=250)
+    args = ap.parse_args()
+    import oracle
+    from hic3defdr_amd import synthetic
+    lib = build()
+    nf = lib.q2qs_fields()
+    names = ('pq cf su ser cf_it su_it ser_it fac_l1 l1_it inv halley wh '
+             'lgam lgam_small lgam_it fit fit_it').split()
+    assert len(names) == nf
+    tmp = tempfile.mkdtemp(prefix='q2qs_')
+    kw = synthetic.write_dataset(tmp, {'chrS': args.bins},
+                                 dist_thresh_max=args.dmax, seed=123)
+    design = kw['design']
+    npz = [p.replace('<chrom>', 'chrS') for p in kw['raw_npz_patterns']]
+    bfs = [p.replace('<chrom>', 'chrS') for p in kw['bias_patterns']]
+    prep = oracle.prepare_chrom(npz, bfs, design, dist_thresh_max=args.dmax)
+    bias = oracle.load_bias(bfs)
+    di = prep['disp_idx']
+    row, col = prep['row'][di], prep['col'][di]
+    raw = np.ascontiguousarray(prep['raw'][di], dtype=np.int32)
+    f = np.ascontiguousarray(bias[row] * bias[col] * prep['size_factors'][di])
+    dist = col - row
+    _, dpd, _ = oracle.estimate_disp([prep], [bias], design,
+                                     dist_thresh_max=args.dmax)
+    order = np.lexsort((raw.sum(1), dist))
+    raw, f, dist = raw[order], np.ascontiguousarray(f[order]), dist[order]
+    n, R = raw.shape
+    cond = design.argmax(axis=1)
+    P = ctypes.c_void_p
+    lib.q2qs_equalize.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P,
+                                  ctypes.c_int, P, P, P]
+    for c in range(design.shape[1]):
+        reps = np.flatnonzero(cond == c).astype(np.int32)
+        nr = len(reps)
+        alpha = np.ascontiguousarray(dpd[dist, c])
+        ok = np.isfinite(alpha)
+        rec = np.zeros((n, nr, nf), dtype=np.int64)
+        out = np.zeros((n, nr))
+        lib.q2qs_equalize(n, R, raw.ctypes.data, f.ctypes.data,
+                          alpha.ctypes.data, nr, reps.ctypes.data,
+                          rec.ctypes.data, out.ctypes.data)
+        rec = rec[ok]
+        m = ok.sum()
+        print('condition %d: %d pixels x %d reps' % (c, m, nr))
+        per = rec.sum(axis=(0, 1)) / (m * nr)
+        for k, v in zip(names, per):
+            print('  %-10s %8.3f / pixel-rep' % (k, v))
+        # wave divergence: lanes = pixels (the rep loop is per lane)
+        w = 64
+        nw = m // w
+        for k in ('cf_it', 'ser_it', 'su_it', 'halley', 'l1_it', 'lgam_it',
+                  'fit_it'):
+            j = names.index(k)
+            v = rec[:nw * w, :, j].sum(1).reshape(nw, w)
+            print('  wave %-8s mean %7.2f  max/mean %5.2f' %
+                  (k, v.mean(), v.max(1).sum() / max(v.sum(1).sum() / w, 1)))
+        # path mix per wave: waves that run both CF and series
+        cfw = rec[:nw * w, :, names.index('cf')].sum(1).reshape(nw, w) > 0
+        sew = (rec[:nw * w, :, names.index('ser')] +
+               rec[:nw * w, :, names.index('su')]).sum(1).reshape(nw, w) > 0
+        print('  waves with both CF and series lanes: %.1f%%' %
+              (100 * np.mean(cfw.any(1) & sew.any(1))))
+        hal = rec[:, :, names.index('halley')].ravel()
+        print('  halley steps histogram:',
+              np.bincount(hal, minlength=9)[:9] / hal.size)
+        fit = rec[:, 0, names.index('fit_it')]
+        print('  fit_mu iterations histogram:',
+              np.bincount(fit, minlength=20)[:20] / fit.size)
+        halley_report(lib, raw, f, dist, dpd, cond, c)
+
+
+
+
+def halley_report(lib, raw, f, dist, dpd, cond, c):
+    P = ctypes.c_void_p
+    n, R = raw.shape
+    reps = np.flatnonzero(cond == c).astype(np.int32)
+    nr = len(reps)
+    alpha = np.ascontiguousarray(dpd[dist, c])
+    out = np.full((n, nr, 6), np.nan)
+    lib.q2qs_halley.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P,
+                                ctypes.c_int, P, P]
+    lib.q2qs_halley(n, R, raw.ctypes.data, f.ctypes.data, alpha.ctypes.data,
+                    nr, reps.ctypes.data, out.ctypes.data)
+    o = out.reshape(-1, 6)
+    o = o[np.isfinite(o[:, 0])]
+    dx1, err1 = o[:, 0], o[:, 3]
+    print('  halley: first-step |dx|/x quantiles 50/90/99/max:',
+          np.quantile(dx1, [.5, .9, .99, 1]))
+    for thr in (1e-6, 1e-5, 1e-4, 1e-3):
+        sel = dx1 <= thr
+        print('   stop after step 1 if dx<=%g: %.1f%% of lanes, max err %.2e'
+              % (thr, 100 * sel.mean(), err1[sel].max() if sel.any() else 0))
+    ratio = err1 / np.maximum(dx1, 1e-300) ** 3
+    print('   err1/dx1^3 quantiles 50/99/max:',
+          np.quantile(ratio[dx1 > 1e-5], [.5, .99, 1]))
+
+
+if __name__ == '__main__':
+    main()
