@@ -53,6 +53,7 @@ struct h3d_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   int n_cu = 256;
+  std::map<const void*, int> resident;  // kernel -> resident workgroups / CU
   bool prof = false;
   std::map<std::string, ProfEntry> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -160,8 +161,28 @@ int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
   return 0;
 }
 
+// workgroups of `kernel` that fit on one CU at once (queried once per kernel;
+// every device of a process is a gfx950)
+template <typename K>
+int resident_blocks(K kernel) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, 0) != hipSuccess ||
+      nb < 1)
+    nb = 1;
+  return nb;
+}
+
+// grid = one full wave of resident workgroups (the kernels grid-stride over
+// the work list), at most one workgroup per item
+template <typename K>
+int work_grid(h3d_ctx* ctx, K kernel, size_t max_items) {
+  int& nb = ctx->resident[(const void*)kernel];
+  if (nb == 0) nb = resident_blocks(kernel);
+  return (int)std::max<size_t>(1, std::min<size_t>(max_items, (size_t)ctx->n_cu * nb));
+}
+
 template <int M>
-void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
+void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                       const double* f_s, double* pd, int64_t n,
                       const int64_t* cs, const int32_t* cl, const int32_t* cd,
                       int C, const int32_t* rep_idx, const int32_t* n_rep,
@@ -170,24 +191,36 @@ void launch_disp_work(h3d_ctx* ctx, int grid, const int32_t* raw_s,
   // equalize pass (heavy: q2qnbinom), then the NLL-only pass (light)
   {
     ProfScope ps(ctx, "disp_work", 0);
-    if (M == 4 && ctx->disp_w == 4)
-      hipLaunchKernelGGL((k_disp_work<M, 4, kEqualize>), dim3(grid), dim3(kBlock), 0,
+    bool done = false;
+    if constexpr (M == 4) {
+      done = true;
+      if (ctx->disp_w == 4) {
+        auto k = k_disp_work<M, 4, kEqualize>;
+        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
+                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
+                           n_rep, st, seg_flags, list, meta, partial);
+      } else if (ctx->disp_w == 3) {
+        auto k = k_disp_work<M, 3, kEqualize>;
+        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
+                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
+                           n_rep, st, seg_flags, list, meta, partial);
+      } else {
+        done = false;
+      }
+    }
+    if (!done) {
+      auto k = k_disp_work<M, 1, kEqualize>;
+      hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
                          ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                         st, seg_flags, list, meta, partial, ctx->work_count);
-    else if (M == 4 && ctx->disp_w == 3)
-      hipLaunchKernelGGL((k_disp_work<M, 3, kEqualize>), dim3(grid), dim3(kBlock), 0,
-                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                         st, seg_flags, list, meta, partial, ctx->work_count);
-    else
-      hipLaunchKernelGGL((k_disp_work<M, 1, kEqualize>), dim3(grid), dim3(kBlock), 0,
-                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                         st, seg_flags, list, meta, partial, ctx->work_count);
+                         st, seg_flags, list, meta, partial);
+    }
   }
   {
     ProfScope ps(ctx, "disp_nll", 0);
-    hipLaunchKernelGGL((k_disp_work<M, 1, kNll>), dim3(grid), dim3(kBlock), 0,
+    auto k = k_disp_work<M, 1, kNll>;
+    hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                       st, seg_flags, list, meta, partial, ctx->work_count);
+                       st, seg_flags, list, meta, partial);
   }
 }
 
@@ -438,6 +471,9 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 
   std::vector<SegState> st(S);
   for (int sg = 0; sg < S; ++sg) seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C]);
+  std::vector<int64_t> lpx(S);
+  for (int d = 0; d < D; ++d)
+    for (int c = 0; c < C; ++c) lpx[d * C + c] = seg_start[d + 1] - seg_start[d];
 
   auto up = [&](const char* slot, const void* src, size_t bytes) -> void* {
     void* p = scratch(ctx, slot, bytes);
@@ -453,17 +489,18 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   int32_t* d_nrep = (int32_t*)up("n_rep", nrep32.data(), C * 4);
   int32_t* d_repidx = (int32_t*)up("rep_idx", rep_idx.data(), rep_idx.size() * 4);
   SegState* d_st = (SegState*)up("seg_state", st.data(), S * sizeof(SegState));
+  int64_t* d_lpx = (int64_t*)up("seg_px", lpx.data(), S * 8);
   const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
   int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
   int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len
   int32_t* d_slb = (int32_t*)scratch(ctx, "seg_lb", S * 4);
   int32_t* d_sle = (int32_t*)scratch(ctx, "seg_le", S * 4);
-  double* d_partial = (double*)scratch(ctx, "partial", max_items * 8);
+  double* d_partial = (double*)scratch(ctx, "partial", max_items * 8 * kWavesPerBlock);
   double* d_total = (double*)scratch(ctx, "seg_total", S * 8);
   int* d_flags = (int*)scratch(ctx, "seg_flags", S * 4);
   double* d_res = (double*)scratch(ctx, "seg_result", S * 8);
   if (!d_cs || !d_cl || !d_cd || !d_scb || !d_sce || !d_nrep || !d_repidx ||
-      !d_st || !d_list || !d_meta || !d_slb || !d_sle || !d_partial ||
+      !d_st || !d_lpx || !d_list || !d_meta || !d_slb || !d_sle || !d_partial ||
       !d_total || !d_flags || !d_res)
     return fail(H3D_ENOMEM, "disp scratch");
   HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));
@@ -471,8 +508,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   // initial active list
   hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                      d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
-                     d_res, d_meta, 1);
-  const int work_grid = std::max(1, std::min<int>((int)max_items, ctx->n_cu * 4));
+                     d_res, d_meta, 1, d_lpx, ctx->work_count);
   int32_t* h_meta = nullptr;
   HIP_TRY(hipHostMalloc((void**)&h_meta, 16, hipHostMallocDefault));
   int rounds = 0, batch = 2, rc = 0;
@@ -481,16 +517,16 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       {
         switch (maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32) {
           case 4:
-            launch_disp_work<4>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<4>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           case 8:
-            launch_disp_work<8>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<8>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           case 16:
-            launch_disp_work<16>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<16>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           default:
-            launch_disp_work<32>(ctx, work_grid, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<32>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
         }
       }
       {
@@ -506,7 +542,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         ProfScope ps(ctx, "disp_update", 0);
         hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                            d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb,
-                           d_sle, d_res, d_meta, 0);
+                           d_sle, d_res, d_meta, 0, d_lpx, ctx->work_count);
       }
       ++rounds;
     }

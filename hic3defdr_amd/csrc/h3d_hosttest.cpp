@@ -27,6 +27,8 @@ extern "C" {
   }
 
 H3DT_UNARY(lgam, lgam)
+H3DT_UNARY(lgam_nll, lgam_nll)
+H3DT_UNARY(log_fast, log_fast)
 H3DT_UNARY(ndtr, ndtr)
 H3DT_UNARY(ndtri, ndtri)
 H3DT_UNARY(log1pmx, log1pmx)

@@ -22,6 +22,14 @@ namespace h3d {
 
 constexpr int kChunk = 256;  // pixels per disp work item (= block size)
 constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / 64;  // disp partials per work item
+
+// deterministic wave sum (fixed butterfly); result valid in every lane
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
 
 // deterministic block sum of one double per thread (fixed butterfly per wave,
 // then waves in order); result valid in thread 0.
@@ -114,7 +122,7 @@ __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
 // Equalize pass: per pixel equalize (scaled_nb.py:186-214) with the
 // segment's current dispersion, write pseudodata, then the NLL term at the
 // first Brent point. NLL pass: the NLL term (dispersion.py:67-70) at the
-// segment's current Brent point. Block partial -> partial[w].
+// segment's current Brent point. Wave partials -> partial[w * 4 + wave].
 // PH = the pass this instantiation runs (kEqualize or kNll): the list holds
 // the equalize items first (meta[2] of them), then the NLL items, and each
 // pass is its own kernel so the light NLL pass is not held to the register
@@ -128,9 +136,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int32_t* __restrict__ n_rep /* C */, const SegState* __restrict__ st,
     int* __restrict__ seg_flags, const int32_t* __restrict__ list,
     const int32_t* __restrict__ meta /* [len, active, eq_len] */,
-    double* __restrict__ partial,
-    unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
-  __shared__ double lds[kBlock / 64];
+    double* __restrict__ partial) {
   const int beg = (PH == kEqualize) ? 0 : meta[2];
   const int end = (PH == kEqualize) ? meta[2] : meta[0];
   for (int w = beg + blockIdx.x; w < end; w += gridDim.x) {
@@ -139,24 +145,22 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int s = chunk_d[chunk] * C + c;
     constexpr int phase = PH;
     const int nr = n_rep[c];
-    if (threadIdx.x == 0)
-      atomicAdd(&work_count[phase == kEqualize ? 0 : 1],
-                (unsigned long long)chunk_len[chunk] * nr);
     double term = 0.0;
     const int i = threadIdx.x;
     if (i < chunk_len[chunk] && nr < 8) {
       // Rolled replicate loop: the q2qnbinom code (the bulk of the kernel)
       // is emitted once instead of once per replicate slot. Sums run
       // sequentially from 0 in replicate order = numpy's row sum for n < 8.
+      constexpr int MS = M < 8 ? M : 8;  // slots for nr < 8
       const int64_t px = chunk_start[chunk] + i;
       const NllConst kc = st[s].k;
       const int32_t* ri = rep_idx + c * kMaxReps;
       double lgsum = 0.0, z = 0.0;
       if (phase == kEqualize) {
         const double alpha = st[s].disp;
-        double x[M], f[M], as[M], lf[M];
+        double x[MS], f[MS], as[MS], lf[MS];
 #pragma unroll
-        for (int k = 0; k < M; ++k) {
+        for (int k = 0; k < MS; ++k) {
           const bool on = k < nr;
           x[k] = on ? (double)raw_s[(int64_t)ri[k] * n + px] : 0.0;
           f[k] = on ? f_s[(int64_t)ri[k] * n + px] : 1.0;
@@ -164,8 +168,8 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           as[k] = alpha;
         }
         int fl = 0;
-        const double f_mean = exp(np_sum<M>(lf, nr) / nr) - 0.0;
-        const double mu = fit_mu<M>(x, f, as, nr, ~0u, &fl);
+        const double f_mean = exp(np_sum<MS>(lf, nr) / nr) - 0.0;
+        const double mu = fit_mu<MS>(x, f, as, nr, ~0u, &fl);
         if (fl) atomicOr(&seg_flags[s], fl);
         const double mu_out0 = mu * f_mean;
         // The reference clamps (mu_in, mu_out) to 0.25 in place and carries
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
         int fc = nr;
         unsigned up = 0u, lo = 0u;
 #pragma unroll
-        for (int k = M - 1; k >= 0; --k)
+        for (int k = MS - 1; k >= 0; --k)
           if (k < nr) {
             const double mi = mu * f[k];
             if (!(mi >= 0.25 && mu_out0 >= 0.25)) fc = k;
@@ -204,23 +208,27 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           double mu_out = (k > fc) ? 0.25 : mu_out0;
           pd[o] = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
         }
-        // NLL term in replicate order (numpy's row sum), from the values
-        // this thread just wrote
+      }
+      // NLL term in replicate order (numpy's row sum) over the pseudodata
+      // (in the equalize pass: the values this thread just wrote). All loads
+      // are issued up front into the slot registers; the rolled loop then
+      // consumes slot 0 and shifts the slots down (static indices only), so
+      // the lgamma code is emitted once and no load latency sits inside it.
+      {
+        double d[MS];
+#pragma unroll
+        for (int k = 0; k < MS; ++k)
+          d[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
 #pragma unroll 1
         for (int k = 0; k < nr; ++k) {
-          const double dk = pd[(int64_t)ri[k] * n + px];
-          lgsum += lgam(dk + kc.r);
-          z += dk;
-        }
-      } else {
-#pragma unroll 1
-        for (int k = 0; k < nr; ++k) {
-          const double dk = pd[(int64_t)ri[k] * n + px];
-          lgsum += lgam(dk + kc.r);
+          const double dk = d[0];
+#pragma unroll
+          for (int j = 0; j + 1 < MS; ++j) d[j] = d[j + 1];
+          lgsum += lgam_nll(dk + kc.r);
           z += dk;
         }
       }
-      term = lgsum + kc.lg_nr - lgam(z + kc.nr) - kc.n_lg_r;
+      term = lgsum + kc.lg_nr - lgam_nll(z + kc.nr) - kc.n_lg_r;
     } else if (M >= 8 && i < chunk_len[chunk]) {
       // >= 8 replicates in the condition: numpy's pairwise row sums
       const int64_t px = chunk_start[chunk] + i;
@@ -253,14 +261,15 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
       const NllConst kc = st[s].k;
       term = nll_pixel<M>(d, nr, kc);
     }
-    const double t = block_sum(term, lds);
-    if (threadIdx.x == 0) partial[w] = t;
-    __syncthreads();
+    // one partial per wave (fixed shuffle tree -> deterministic); no block
+    // barrier, so the waves of a block run their items independently
+    const double t = wave_sum(term);
+    if ((threadIdx.x & 63) == 0) partial[(int64_t)w * kWavesPerBlock + (threadIdx.x >> 6)] = t;
   }
 }
 
-// seg_total[s] = sum of the segment's partials in list order (one wave per
-// segment, fixed reduction tree -> deterministic)
+// seg_total[s] = sum of the segment's wave partials in list order (one wave
+// per segment, fixed reduction tree -> deterministic)
 __global__ void k_seg_reduce(const double* __restrict__ partial,
                              const int32_t* __restrict__ seg_lb,
                              const int32_t* __restrict__ seg_le, int S,
@@ -268,9 +277,10 @@ __global__ void k_seg_reduce(const double* __restrict__ partial,
   const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (s >= S) return;
-  const int b = seg_lb[s], e = seg_le[s];
+  const int64_t b = (int64_t)seg_lb[s] * kWavesPerBlock,
+                e = (int64_t)seg_le[s] * kWavesPerBlock;
   double v = 0.0;
-  for (int j = b + lane; j < e; j += 64) v += partial[j];
+  for (int64_t j = b + lane; j < e; j += 64) v += partial[j];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   if (lane == 0) seg_total[s] = v;
@@ -285,12 +295,20 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     const int32_t* __restrict__ seg_chunk_e, int32_t* __restrict__ list,
     int32_t* __restrict__ seg_lb,
     int32_t* __restrict__ seg_le, double* __restrict__ result,
-    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first) {
+    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first,
+    const int64_t* __restrict__ seg_px /* this rank's pixels per segment */,
+    unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
   __shared__ int32_t scan[1024];
   __shared__ int32_t base_s;
-  if (threadIdx.x == 0) base_s = 0;
+  __shared__ unsigned long long wc[2];
+  if (threadIdx.x == 0) {
+    base_s = 0;
+    wc[0] = wc[1] = 0ull;
+  }
   __syncthreads();
-  // advance the state machines
+  // advance the state machines; count the pixel-replicates the next round's
+  // passes will visit (measurement: algorithmic bytes of the disp kernels)
+  unsigned long long weq = 0ull, wnll = 0ull;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     SegState cur = st[s];
     if (!first && cur.phase != kDone) {
@@ -299,8 +317,17 @@ __global__ __launch_bounds__(1024) void k_seg_update(
       st[s] = cur;
     }
     if (cur.phase == kDone) result[s] = cur.result;
+    const unsigned long long w = (unsigned long long)seg_px[s] * n_rep[s % C];
+    if (cur.phase == kEqualize) weq += w;
+    if (cur.phase == kNll) wnll += w;
   }
+  if (weq) atomicAdd(&wc[0], weq);
+  if (wnll) atomicAdd(&wc[1], wnll);
   __syncthreads();
+  if (threadIdx.x == 0) {
+    work_count[0] += wc[0];
+    work_count[1] += wc[1];
+  }
   // list: equalize items of every segment first, then the NLL items
   for (int pass = 0; pass < 2; ++pass) {
   const int want = pass == 0 ? kEqualize : kNll;

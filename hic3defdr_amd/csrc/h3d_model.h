@@ -379,14 +379,16 @@ H3D_HD NllConst nll_const(double delta, int n) {
 }
 
 // one pixel's term sum_k gammaln(d_k + r) + gammaln(n r) - gammaln(z + n r)
-// - n gammaln(r); nll(delta) = -(sum over pixels).
+// - n gammaln(r); nll(delta) = -(sum over pixels). The per-pixel gammaln
+// terms use lgam_nll (absolute error ~1e-15, far below the rounding of the
+// segment sum), the per-segment constants cephes lgam.
 template <int M>
 H3D_HD double nll_pixel(const double* d, int n, const NllConst& k) {
   double lg[M];
 #pragma unroll
-  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam(d[j] + k.r) : 0.0;
+  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam_nll(d[j] + k.r) : 0.0;
   const double z = np_sum<M>(d, n);
-  return np_sum<M>(lg, n) + k.lg_nr - lgam(z + k.nr) - k.n_lg_r;
+  return np_sum<M>(lg, n) + k.lg_nr - lgam_nll(z + k.nr) - k.n_lg_r;
 }
 
 // ---- qcml + bounded Brent as a resumable state machine --------------------

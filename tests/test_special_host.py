@@ -192,3 +192,18 @@ def test_log1pmx_fixed_length_form(lib):
     assert rel_err(got[:3000], ref) < 4e-16 * 8
     big = np.abs(x) > 1e-3  # where log1p(x) - x itself is still accurate
     assert rel_err(got[big], np.log1p(x[big]) - x[big]) < 1e-10
+
+
+def test_lgam_nll_and_log_fast(lib):
+    # the NLL-sum lgamma: absolute error bound (each term joins a sum of
+    # thousands), checked against scipy gammaln over the NLL argument range
+    # d + r, r = 1/delta - 1 in [0.0101, 9999]
+    rng = np.random.default_rng(11)
+    x = np.concatenate([10 ** rng.uniform(np.log10(0.0101), 6, 40000),
+                        rng.uniform(0.0101, 14, 40000)])
+    got = unary(lib, 'lgam_nll', x)
+    ref = sc.gammaln(x)
+    assert np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref))) < 8e-15
+    assert np.isinf(unary(lib, 'lgam_nll', np.array([np.inf])))[0]
+    v = 10 ** rng.uniform(-300, 300, 40000)
+    assert rel_err(unary(lib, 'log_fast', v), np.log(v)) < 4e-16
