@@ -259,15 +259,22 @@ H3D_HD double igam_fac_l(double a, double x, double lga) {
 
 H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
 
-// power series sum of P(a, x) = fac / a * sum (DLMF 8.11.4)
+// power series sum of P(a, x) = fac / a * sum (DLMF 8.11.4), two terms per
+// division: c_{n} = c_{n-1} x / (a+n) = c_{n-1} x (a+n+1) / ((a+n)(a+n+1)).
+// Stops at the first term <= eps * sum, as cephes igam_series.
 H3D_HD double igam_series_sum(double a, double x) {
   double r = a, c = 1.0, ans = 1.0;
-  for (int i = 0; i < kMaxIter; ++i) {
-    H3D_STAT(ser_it, 1);
-    r += 1.0;
-    c *= x / r;
+  for (int i = 0; i < kMaxIter / 2; ++i) {
+    H3D_STAT(ser_it, 2);
+    const double r1 = r + 1.0, r2 = r + 2.0;
+    const double xi = x / (r1 * r2);
+    c *= xi * r2;
     ans += c;
     if (c <= kMachEp * ans) break;
+    c *= xi * r1;
+    ans += c;
+    if (c <= kMachEp * ans) break;
+    r = r2;
   }
   return ans;
 }
@@ -298,27 +305,27 @@ H3D_HD double igamc_series(double a, double x) {
   return igamc_series_l(a, x, lgam(a));
 }
 
-// continued-fraction value of Q(a, x) / fac (DLMF 8.9.2)
+// continued-fraction value of Q(a, x) / fac (DLMF 8.9.2), cephes igamc's
+// recurrence without the two divisions per step: consecutive convergents
+// p_{k-1}/q_{k-1}, p_k/q_k are compared by cross-multiplication,
+//   |p_k q_{k-1} - p_{k-1} q_k| <= tol |p_k q_{k-1}|,
+// and the quotient is formed once at the end. tol = 4 eps: the fused
+// cross product is exact to ~1 eps of |p_k q_{k-1}|, so the test is met once
+// the convergents agree to ~3 eps (cephes: once they round to the same double).
 H3D_HD double igamc_cf_ratio(double a, double x) {
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
   double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
-  double ans = pkm1 / qkm1;
   for (int i = 0; i < kMaxIter; ++i) {
     H3D_STAT(cf_it, 1);
     c += 1.0;
     y += 1.0;
     z += 2.0;
-    double yc = y * c;
-    double pk = pkm1 * z - pkm2 * yc;
-    double qk = qkm1 * z - qkm2 * yc;
-    double t;
-    if (qk != 0.0) {
-      double r = pk / qk;
-      t = fabs((ans - r) / r);
-      ans = r;
-    } else {
-      t = 1.0;
-    }
+    const double yc = y * c;
+    const double pk = pkm1 * z - pkm2 * yc;
+    const double qk = qkm1 * z - qkm2 * yc;
+    const double lead = pk * qkm1;
+    const double cross = lead - pkm1 * qk;
+    const bool done = (qk != 0.0) && fabs(cross) <= 4.0 * kMachEp * fabs(lead);
     pkm2 = pkm1;
     pkm1 = pk;
     qkm2 = qkm1;
@@ -329,9 +336,9 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
       qkm2 *= kBigInv;
       qkm1 *= kBigInv;
     }
-    if (t <= kMachEp) break;
+    if (done) break;
   }
-  return ans;
+  return pkm1 / qkm1;
 }
 
 // Q(a, x) by the continued fraction.
