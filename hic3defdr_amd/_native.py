@@ -248,8 +248,11 @@ class Context(object):
             'h3d_lrt_dev')
 
     # -- measurement ---------------------------------------------------------
-    def profile(self, on=True):
-        _check(self.lib.h3d_profile_enable(self.handle, int(on)),
+    def profile(self, on=True, level=2):
+        """HIP-event timing on the ctx stream: level 1 = the roofline
+        kernels only (disp_work, lrt), 2 = every kernel scope."""
+        _check(self.lib.h3d_profile_enable(self.handle,
+                                           int(level) if on else 0),
                'h3d_profile_enable')
 
     def profile_reset(self):

@@ -54,7 +54,10 @@ struct h3d_ctx {
   hipStream_t stream = nullptr;
   int n_cu = 256;
   std::map<const void*, int> resident;  // kernel -> resident workgroups / CU
-  bool prof = false;
+  // 0 off; 1: the roofline kernels only ("disp_work", "lrt"); 2: every
+  // scope. Events are collected lazily (profile_read / reset / close), so
+  // the launch path never waits on them.
+  int prof = 0;
   std::map<std::string, ProfEntry> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<int64_t> pending_units;
@@ -98,27 +101,35 @@ hipEvent_t ev_get(h3d_ctx* ctx) {
   return e;
 }
 
+void prof_collect(h3d_ctx* ctx);
+
 // wraps one kernel launch with HIP events on the ctx stream when profiling
 struct ProfScope {
   h3d_ctx* ctx;
   const char* name;
   int64_t units;
   hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(h3d_ctx* c, const char* n, int64_t u) : ctx(c), name(n), units(u) {
-    if (ctx->prof) {
+  bool on;
+  ProfScope(h3d_ctx* c, const char* n, int64_t u, int level = 2)
+      : ctx(c), name(n), units(u), on(c->prof >= level) {
+    // bound the pending list (collecting synchronises the stream)
+    if (on && ctx->pending.size() > 16384) prof_collect(ctx);
+    if (on) {
       a = ev_get(ctx);
       b = ev_get(ctx);
       (void)hipEventRecord(a, ctx->stream);
     }
   }
   ~ProfScope() {
-    if (ctx->prof) {
+    if (on) {
       (void)hipEventRecord(b, ctx->stream);
       ctx->pending.push_back({name, {a, b}});
       ctx->pending_units.push_back(units);
     }
   }
 };
+
+
 
 void prof_collect(h3d_ctx* ctx) {
   if (ctx->pending.empty()) return;
@@ -190,7 +201,7 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                       const int32_t* meta, double* partial) {
   // equalize pass (heavy: q2qnbinom), then the NLL-only pass (light)
   {
-    ProfScope ps(ctx, "disp_work", 0);
+    ProfScope ps(ctx, "disp_work", 0, 1);
     bool done = false;
     if constexpr (M == 4) {
       done = true;
@@ -334,7 +345,7 @@ int h3d_set_stream(h3d_ctx* ctx, void* stream) {
 int h3d_profile_enable(h3d_ctx* ctx, int on) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   prof_collect(ctx);
-  ctx->prof = on != 0;
+  ctx->prof = on < 0 ? 0 : on > 2 ? 2 : on;
   return 0;
 }
 
@@ -563,7 +574,6 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   (void)hipHostFree(h_meta);
   if (rc) return rc;
-  prof_collect(ctx);
   std::vector<int32_t> fl(S);
   HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(st.data(), d_st, S * sizeof(SegState), hipMemcpyDeviceToHost, s));
@@ -662,7 +672,7 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
   const int grid = grid_for(ctx, n, 16);
   {
-    ProfScope ps(ctx, "lrt", n);
+    ProfScope ps(ctx, "lrt", n, 1);
     const int m = R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
     const int cm = C <= 2 ? 2 : C <= 4 ? 4 : 8;
 #define H3D_LRT(MM, CC)                                                          \

@@ -20,6 +20,8 @@
 #include <numeric>
 #include <vector>
 
+// No FMA contraction in the host numerics (the tables must match the
+// reference's bits). libh3d keeps it off for the kernels too (h3d_special.h).
 #pragma clang fp contract(off)
 
 namespace h3dhost {

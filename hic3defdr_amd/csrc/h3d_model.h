@@ -442,6 +442,11 @@ H3D_HD double sgn(double v) { return (double)((v > 0) - (v < 0)); }
 
 // Advance with the NLL pixel-term total evaluated at s->x.
 H3D_HD void seg_step(SegState* s, double total, int n_reps) {
+#if defined(__clang__)
+  // scipy's Brent arithmetic op for op (no fused multiply-adds): the trial
+  // points follow the reference bit for bit given the same NLL values
+#pragma clang fp contract(off)
+#endif
   const double sqrt_eps = brent_sqrt_eps();
   const double golden_mean = brent_golden();
   const double fval = -total;

@@ -19,6 +19,16 @@
 #include <cmath>
 #include <cstdint>
 
+// FMA contraction off for everything built on these headers: it keeps the
+// device arithmetic op-for-op with the host test build (g++
+// -ffp-contract=off), and measured on gfx950 (r01) contracting the
+// q2qnbinom / incomplete-gamma code raised the equalize kernel's register
+// demand (W=4 budget: 128 -> 384 B of spills) and cost 8% (11.7 -> 12.6 ms
+// per bench step).
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
 #if defined(__HIPCC__)
 #define H3D_HD __host__ __device__ inline
 #else
@@ -34,13 +44,23 @@ struct Stats {
       lgam, lgam_small, lgam_it, fit, fit_it;
 };
 inline thread_local Stats* g_stats = nullptr;
+inline thread_local double* g_pq_log = nullptr;  // (a, x, iterations, path)
+inline thread_local int64_t g_pq_cap = 0, g_pq_n = 0;
+inline void pq_log(double a, double x, long it, int path) {
+  if (g_pq_log && g_pq_n < g_pq_cap) {
+    double* o = g_pq_log + 4 * g_pq_n++;
+    o[0] = a, o[1] = x, o[2] = (double)it, o[3] = path;
+  }
+}
 }  // namespace h3d
+#define H3D_PQ_LOG(a, x, it, path) h3d::pq_log(a, x, it, path)
 #define H3D_STAT(field, v) \
   do {                     \
     if (h3d::g_stats) h3d::g_stats->field += (v); \
   } while (0)
 #else
 #define H3D_STAT(field, v) ((void)0)
+#define H3D_PQ_LOG(a, x, it, path) ((void)0)
 #endif
 
 namespace h3d {
@@ -362,6 +382,9 @@ H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
   // compiler keep them in a dynamically indexed scratch pair)
   double v;
   bool is_q;
+#if defined(H3D_INSTRUMENT) && !defined(__HIP_DEVICE_COMPILE__)
+  const long it0 = g_stats ? g_stats->cf_it + g_stats->su_it + g_stats->ser_it : 0;
+#endif
   if (x > 1.0 && x > a) {  // continued fraction for the upper tail
     H3D_STAT(cf, 1);
     v = (f == 0.0) ? 0.0 : igamc_cf_ratio(a, x) * f;
@@ -377,6 +400,11 @@ H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
     v = (f == 0.0) ? 0.0 : igam_series_sum(a, x) * f / a;
     is_q = false;
   }
+#if defined(H3D_INSTRUMENT) && !defined(__HIP_DEVICE_COMPILE__)
+  if (g_stats)
+    H3D_PQ_LOG(a, x, g_stats->cf_it + g_stats->su_it + g_stats->ser_it - it0,
+               (x > 1.0 && x > a) ? 0 : is_q ? 1 : 2);
+#endif
   const double w = 1.0 - v;
   *P = is_q ? w : v;
   *Q = is_q ? v : w;

@@ -141,7 +141,9 @@ int h3d_bh(const double* p, int64_t n, double* q);
 
 /* ---- measurement -------------------------------------------------------- */
 
-/* Per-kernel HIP-event timing on the ctx stream. name in {"disp_work" (the
+/* Per-kernel HIP-event timing on the ctx stream; on = 0 off, 1 the roofline
+ * kernels only ("disp_work", "lrt"), 2 every scope. Events are read back
+ * lazily (profile_read / profile_reset). name in {"disp_work" (the
  * equalize pass), "disp_nll", "disp_reduce", "disp_update", "disp_prep",
  * "lrt"}. units: algorithmic HBM bytes for "disp_work" / "disp_nll"
  * (counted on the device since the last reset), pixels for "lrt" /

@@ -158,3 +158,45 @@ void q2qs_fit_trace(int n, const double* x, const double* b, double a) {
   fflush(stdout);
 }
 }
+
+extern "C" {
+// per igam_pq call log for one equalize sweep: (a, x, iterations, path)
+// path 0 = CF, 1 = small-x upper series, 2 = power series. Returns count.
+int64_t q2qs_pq_log(int64_t n, int R, const int32_t* raw, const double* f,
+                    const double* alpha, int nr, const int32_t* rep_idx,
+                    double* out /* (cap, 4) */, int64_t cap) {
+  using namespace h3d;
+  constexpr int M = 8;
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n && cnt + 64 < cap; ++i) {
+    double x[M], fs[M], as[M], lf[M];
+    for (int k = 0; k < M; ++k) {
+      const bool on = k < nr;
+      x[k] = on ? raw[i * R + rep_idx[k]] : 0.0;
+      fs[k] = on ? f[i * R + rep_idx[k]] : 1.0;
+      lf[k] = on ? log(fs[k]) : 0.0;
+      as[k] = alpha[i];
+    }
+    if (!(alpha[i] > 0)) continue;
+    int fl = 0;
+    const double f_mean = exp(np_sum<M>(lf, nr) / nr);
+    const double mu = fit_mu<M>(x, fs, as, nr, ~0u, &fl);
+    double mu_out = mu * f_mean;
+    LgamCache cache;
+    for (int k = 0; k < nr; ++k) {
+      double mu_in = mu * fs[k];
+      Stats st;
+      memset(&st, 0, sizeof st);
+      g_stats = &st;
+      g_pq_log = out + cnt * 4;
+      g_pq_cap = cap - cnt;
+      g_pq_n = 0;
+      (void)q2q(x[k], &mu_in, &mu_out, alpha[i], &cache);
+      cnt += g_pq_n;
+      g_pq_log = nullptr;
+      g_stats = nullptr;
+    }
+  }
+  return cnt;
+}
+}

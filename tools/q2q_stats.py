@@ -101,6 +101,7 @@ def main():
         print('  fit_mu iterations histogram:',
               np.bincount(fit, minlength=20)[:20] / fit.size)
         halley_report(lib, raw, f, dist, dpd, cond, c)
+        pq_report(lib, raw, f, dist, dpd, cond, c)
 
 
 
@@ -128,6 +129,32 @@ def halley_report(lib, raw, f, dist, dpd, cond, c):
     ratio = err1 / np.maximum(dx1, 1e-300) ** 3
     print('   err1/dx1^3 quantiles 50/99/max:',
           np.quantile(ratio[dx1 > 1e-5], [.5, .99, 1]))
+
+
+def pq_report(lib, raw, f, dist, dpd, cond, c):
+    P = ctypes.c_void_p
+    n, R = raw.shape
+    reps = np.flatnonzero(cond == c).astype(np.int32)
+    alpha = np.ascontiguousarray(dpd[dist, c])
+    cap = n * len(reps) * 6
+    out = np.zeros((cap, 4))
+    lib.q2qs_pq_log.restype = ctypes.c_int64
+    lib.q2qs_pq_log.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P,
+                                ctypes.c_int, P, P, ctypes.c_int64]
+    m = lib.q2qs_pq_log(n, R, raw.ctypes.data, f.ctypes.data,
+                        alpha.ctypes.data, len(reps), reps.ctypes.data,
+                        out.ctypes.data, cap)
+    a, x, it, path = out[:m].T
+    print('  pq calls %d, mean iterations %.1f' % (m, it.mean()))
+    for lo, hi in ((0, 1), (1, 5), (5, 20), (20, 100), (100, 1e9)):
+        sel = (a >= lo) & (a < hi)
+        print('   a in [%g, %g): %.1f%% of calls, %.1f%% of iterations, '
+              'mean it %.1f' % (lo, hi, 100 * sel.mean(),
+                                100 * it[sel].sum() / it.sum(),
+                                it[sel].mean() if sel.any() else 0))
+    temme = (a > 20) & (np.abs(x - a) / a < 0.3)
+    print('   Temme region (a>20, |x-a|/a<0.3): %.1f%% of calls, %.1f%% of '
+          'iterations' % (100 * temme.mean(), 100 * it[temme].sum() / it.sum()))
 
 
 if __name__ == '__main__':
