@@ -230,7 +230,7 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha,
     tg = right ? 1.0 : 0.0;
   } else {
     double P, Q, fac;
-    igam_pq(a_in, xs, lgam(a_in), &P, &Q, &fac);
+    igam_pq(a_in, xs, lgam(a_in), &P, &Q, &fac, right ? 1 : 0);
     tg = right ? Q : P;
   }
   double qg;

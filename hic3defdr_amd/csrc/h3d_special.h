@@ -372,8 +372,13 @@ H3D_HD double igamc_cf(double a, double x) {
 // lga = lgam(a) (a > 0, x > 0 finite). The branch structure follows cephes
 // igam/igamc: the tail that is computed directly is the accurate one, the
 // other is 1 - it.
+// tail = 1 / 0: the caller needs Q / P accurately. Then the method that
+// computes that tail directly is used wherever it converges well -- the
+// continued fraction for Q whenever x > 1, the power series for P up to
+// x < 1.5 a + 5 -- instead of cephes' x-vs-a switch, so lanes of a wave that
+// want the same tail take the same branch. tail = -1: the cephes rule.
 H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
-                    double* fac) {
+                    double* fac, int tail = -1) {
   H3D_STAT(pq, 1);
   const double f = igam_fac_l(a, x, lga);
   *fac = f;
@@ -385,7 +390,10 @@ H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
 #if defined(H3D_INSTRUMENT) && !defined(__HIP_DEVICE_COMPILE__)
   const long it0 = g_stats ? g_stats->cf_it + g_stats->su_it + g_stats->ser_it : 0;
 #endif
-  if (x > 1.0 && x > a) {  // continued fraction for the upper tail
+  const bool use_cf = (tail == 1)   ? x > 1.0
+                     : (tail == 0) ? (x > 1.0 && x > a && !(x < 1.5 * a + 5.0))
+                                   : (x > 1.0 && x > a);
+  if (use_cf) {  // continued fraction for the upper tail
     H3D_STAT(cf, 1);
     v = (f == 0.0) ? 0.0 : igamc_cf_ratio(a, x) * f;
     is_q = true;
@@ -403,7 +411,7 @@ H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
 #if defined(H3D_INSTRUMENT) && !defined(__HIP_DEVICE_COMPILE__)
   if (g_stats)
     H3D_PQ_LOG(a, x, g_stats->cf_it + g_stats->su_it + g_stats->ser_it - it0,
-               (x > 1.0 && x > a) ? 0 : is_q ? 1 : 2);
+               use_cf ? 0 : is_q ? 1 : 2);
 #endif
   const double w = 1.0 - v;
   *P = is_q ? w : v;
@@ -656,7 +664,7 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
   for (int i = 0; i < 8; ++i) {
     H3D_STAT(halley, 1);
     double P, Q, fac;
-    igam_pq(a, x, lga, &P, &Q, &fac);
+    igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
     if (fac == 0.0) return x;
     const double f_fp = upper ? (Q - t) * x / (-fac) : (P - t) * x / fac;
     const double fpp_fp = -1.0 + (a - 1) / x;

@@ -200,3 +200,66 @@ int64_t q2qs_pq_log(int64_t n, int R, const int32_t* raw, const double* f,
   return cnt;
 }
 }
+
+extern "C" {
+// Per pixel and replicate slot, in the kernel's visiting order (upper tail
+// first): the igam_pq calls of q2qnbinom -- count, then (iterations, path)
+// of up to 5 calls; plus fit_mu iterations per pixel. rec: (n, nr, 11),
+// fit: (n).
+void q2qs_wave_log(int64_t n, int R, const int32_t* raw, const double* f,
+                   const double* alpha, int nr, const int32_t* rep_idx,
+                   double* rec, double* fit) {
+  using namespace h3d;
+  constexpr int M = 8;
+  double buf[4 * 16];
+  for (int64_t i = 0; i < n; ++i) {
+    double x[M], fs[M], as[M], lf[M];
+    for (int k = 0; k < M; ++k) {
+      const bool on = k < nr;
+      x[k] = on ? raw[i * R + rep_idx[k]] : 0.0;
+      fs[k] = on ? f[i * R + rep_idx[k]] : 1.0;
+      lf[k] = on ? log(fs[k]) : 0.0;
+      as[k] = alpha[i];
+    }
+    for (int j = 0; j < nr * 11; ++j) rec[i * nr * 11 + j] = 0.0;
+    fit[i] = 0.0;
+    if (!(alpha[i] > 0)) continue;
+    Stats st;
+    memset(&st, 0, sizeof st);
+    g_stats = &st;
+    int fl = 0;
+    const double f_mean = exp(np_sum<M>(lf, nr) / nr);
+    const double mu = fit_mu<M>(x, fs, as, nr, ~0u, &fl);
+    fit[i] = (double)st.fit_it;
+    const double mu_out0 = mu * f_mean;
+    int fc = nr;
+    unsigned up = 0u, lo = 0u;
+    for (int k = nr - 1; k >= 0; --k) {
+      const double mi = mu * fs[k];
+      if (!(mi >= 0.25 && mu_out0 >= 0.25)) fc = k;
+      if (x[k] >= mi) up |= 1u << k; else lo |= 1u << k;
+    }
+    LgamCache cache;
+    for (int j = 0; j < nr; ++j) {
+      int k;
+      if (up) { k = __builtin_ctz(up); up &= up - 1u; }
+      else { k = __builtin_ctz(lo); lo &= lo - 1u; }
+      double mu_in = mu * fs[k];
+      double mu_out = (k > fc) ? 0.25 : mu_out0;
+      memset(&st, 0, sizeof st);
+      g_pq_log = buf;
+      g_pq_cap = 16;
+      g_pq_n = 0;
+      (void)q2q(x[k], &mu_in, &mu_out, alpha[i], &cache);
+      double* o = rec + (i * nr + j) * 11;
+      o[0] = (double)g_pq_n;
+      for (int c = 0; c < 5 && c < g_pq_n; ++c) {
+        o[1 + 2 * c] = buf[4 * c + 2];
+        o[2 + 2 * c] = buf[4 * c + 3];
+      }
+      g_pq_log = nullptr;
+    }
+    g_stats = nullptr;
+  }
+}
+}

@@ -102,6 +102,7 @@ def main():
               np.bincount(fit, minlength=20)[:20] / fit.size)
         halley_report(lib, raw, f, dist, dpd, cond, c)
         pq_report(lib, raw, f, dist, dpd, cond, c)
+        wave_report(lib, raw, f, dist, dpd, cond, c)
 
 
 
@@ -155,6 +156,62 @@ def pq_report(lib, raw, f, dist, dpd, cond, c):
     temme = (a > 20) & (np.abs(x - a) / a < 0.3)
     print('   Temme region (a>20, |x-a|/a<0.3): %.1f%% of calls, %.1f%% of '
           'iterations' % (100 * temme.mean(), 100 * it[temme].sum() / it.sum()))
+
+
+def wave_report(lib, raw, f, dist, dpd, cond, c, it_cost=18.0,
+                call_cost=250.0, fit_cost=60.0):
+    """Wave-level cost model of the equalize kernel: per slot, each pq-call
+    position costs max-over-lanes iterations * it_cost (+ call_cost if any
+    lane makes the call); fit_mu max iterations * fit_cost. Compared with
+    the lane-mean (perfect utilisation)."""
+    P = ctypes.c_void_p
+    n, R = raw.shape
+    reps = np.flatnonzero(cond == c).astype(np.int32)
+    nr = len(reps)
+    alpha = np.ascontiguousarray(dpd[dist, c])
+    rec = np.zeros((n, nr, 11))
+    fit = np.zeros(n)
+    lib.q2qs_wave_log.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P,
+                                  ctypes.c_int, P, P, P]
+    lib.q2qs_wave_log(n, R, raw.ctypes.data, f.ctypes.data, alpha.ctypes.data,
+                      nr, reps.ctypes.data, rec.ctypes.data, fit.ctypes.data)
+    ok = np.isfinite(alpha) & (alpha > 0)
+    rec, fit = rec[ok], fit[ok]
+    w = 64
+    nw = len(rec) // w
+    rec = rec[:nw * w].reshape(nw, w, nr, 11)
+    fit = fit[:nw * w].reshape(nw, w)
+    parts = {}
+    ncall = rec[..., 0]
+    its = rec[..., 1::2]          # (nw, w, nr, 5)
+    paths = rec[..., 2::2]
+    made = np.arange(5)[None, None, None, :] < ncall[..., None]
+    itm = np.where(made, its, 0)
+    # actual: per slot j, call position c: max over lanes; CF and series
+    # paths diverge -> pay both maxima
+    cf = np.where(made & (paths == 0), itm, 0)
+    se = np.where(made & (paths != 0), itm, 0)
+    act_it = (cf.max(1) + se.max(1)).sum(axis=(1, 2)) * it_cost
+    act_call = made.any(1).sum(axis=(1, 2)) * call_cost
+    act_fit = fit.max(1) * fit_cost
+    ideal_it = itm.sum(axis=(1, 2, 3)) / w * it_cost
+    ideal_call = made.sum(axis=(1, 2, 3)) / w * call_cost
+    ideal_fit = fit.mean(1) * fit_cost
+    print('  wave model (cost units / wave): iterations %.0f (ideal %.0f), '
+          'call overhead %.0f (ideal %.0f), fit %.0f (ideal %.0f)' % (
+              act_it.mean(), ideal_it.mean(), act_call.mean(),
+              ideal_call.mean(), act_fit.mean(), ideal_fit.mean()))
+    # by call position
+    for cpos in range(4):
+        a = (cf[..., cpos].max(1) + se[..., cpos].max(1)).sum(1).mean()
+        b = itm[..., cpos].sum(axis=(1, 2)).mean() / w
+        frac = made[..., cpos].mean()
+        both = ((cf[..., cpos] > 0).any(1) & (se[..., cpos] > 0).any(1)).mean()
+        print('   call %d: lanes making it %.2f, wave iters %.1f vs mean %.1f,'
+              ' slot-waves with both paths %.2f' % (cpos, frac, a, b, both))
+    tot = act_it + act_call + act_fit
+    ideal = ideal_it + ideal_call + ideal_fit
+    print('  modelled lane utilisation %.2f' % (ideal.sum() / tot.sum()))
 
 
 if __name__ == '__main__':
