@@ -24,6 +24,7 @@ EXPORTS = [
     'h3d_size_factors_cmor', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
     'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
+    'h3d_find_clusters', 'h3d_format_clusters',
 ]
 
 
@@ -77,6 +78,9 @@ def load_library(path=None):
             'h3d_profile_enable': (_I, [_P, _I]),
             'h3d_profile_read': (_I, [_P, ctypes.c_char_p, _P, _P, _P]),
             'h3d_profile_reset': (_I, [_P]),
+            'h3d_find_clusters': (_I, [_P, _P, _I64, _I, _P, _P]),
+            'h3d_format_clusters': (_I, [_P, _P, _P, _P, _I64, _P, _I64, _P,
+                                         _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -288,6 +292,40 @@ def bh(pvalues):
     q = np.empty_like(p)
     _check(lib.h3d_bh(_ptr(p), len(p), _ptr(q)), 'h3d_bh')
     return q
+
+
+def cluster_labels(row, col, connectivity=1):
+    """Cluster index of every pixel, clusters numbered in the reference's
+    get_groups() order (libh3d host code, clusters.py:73-97)."""
+    lib = load_library()
+    r = _c(row, np.int64)
+    c = _c(col, np.int64)
+    lab = np.empty(len(r), dtype=np.int64)
+    nc = ctypes.c_int64(0)
+    _check(lib.h3d_find_clusters(_ptr(r), _ptr(c), len(r), int(connectivity),
+                                 _ptr(lab), ctypes.byref(nc)),
+           'h3d_find_clusters')
+    return lab, nc.value
+
+
+def format_clusters(row, col, members, starts):
+    """Text "[[i, j], ...]" of each cluster -> (bytes, end offsets)."""
+    lib = load_library()
+    r = _c(row, np.int64)
+    c = _c(col, np.int64)
+    m = _c(members, np.int64)
+    s = _c(starts, np.int64)
+    k = len(s) - 1
+    ln = ctypes.c_int64(0)
+    _check(lib.h3d_format_clusters(_ptr(r), _ptr(c), _ptr(m), _ptr(s), k,
+                                   None, 0, None, ctypes.byref(ln)),
+           'h3d_format_clusters')
+    buf = ctypes.create_string_buffer(max(ln.value, 1))
+    ends = np.empty(k, dtype=np.int64)
+    _check(lib.h3d_format_clusters(_ptr(r), _ptr(c), _ptr(m), _ptr(s), k,
+                                   buf, ln.value, _ptr(ends),
+                                   ctypes.byref(ln)), 'h3d_format_clusters')
+    return buf.raw[:ln.value], ends
 
 
 _ctx = {}

@@ -9,17 +9,27 @@ work runs on the GPU through libh3d.so:
                    h3d_disp_table (lowess smoother, host C++ in libh3d)
   lrt           -> h3d_lrt (fused per-pixel NB GLM fits + LRT + chi2)
   bh            -> h3d_bh
+  threshold / classify / collect
+                -> h3d_find_clusters + h3d_format_clusters (host C++ in
+                   libh3d: the reference's DirectedDisjointSet clustering and
+                   the cluster JSON / TSV text)
 
 ``n_threads`` is accepted for signature compatibility: the reference's
 process pools (util/parallelization.py) are replaced by the GPU; multi-GPU
 sharding is hic3defdr_amd.parallel.
 """
+import os
+
 import numpy as np
 import scipy.sparse as sparse
 
 from hic3defdr_amd import _native
 from hic3defdr_amd.analysis.core import DispFn
-from hic3defdr_amd.util.clusters import load_clusters, pixel_membership
+from hic3defdr_amd.util.classification import classify_clusters
+from hic3defdr_amd.util.cluster_table import ClusterTable
+from hic3defdr_amd.util.clusters import (load_clusters, load_cluster_list,
+                                         pixel_membership, save_clusters)
+from hic3defdr_amd.util.thresholding import threshold_clusters
 from hic3defdr_amd.util.printing import eprint
 
 NATIVE_NORMS = ('conditional_mor',)
@@ -197,3 +207,95 @@ class AnalyzingHiC3DeFDR(object):
                            n_threads=n_threads)
         self.lrt(refit_mu=refit_mu, n_threads=n_threads, verbose=verbose)
         self.bh()
+
+    # ------------------------------------------------------------------
+    def _chroms_for(self, chrom):
+        return self.chroms if chrom is None else [chrom]
+
+    def threshold(self, chrom=None, fdr=0.05, cluster_size=3, n_threads=-1):
+        """Reference ``analysis.py:366-431``: sig / insig clusters per FDR
+        and cluster size -> ``sig_<fdr>_<size>_<chrom>.json`` (+ ``.tsv``
+        when ``res`` is set), same for ``insig``."""
+        fdrs = list(fdr) if hasattr(fdr, '__len__') else [fdr]
+        sizes = list(cluster_size) if hasattr(cluster_size, '__len__') \
+            else [cluster_size]
+        for ch in self._chroms_for(chrom):
+            eprint('thresholding and clustering chrom %s' % ch)
+            row, col, q = self.load_data('qvalues', ch, coo=True)
+            for f in fdrs:
+                sig, insig = threshold_clusters(q, row, col, f)
+                for s in sizes:
+                    for kind, cl in (('sig', sig), ('insig', insig)):
+                        kept = cl.size_filter(s)
+                        out = '%s/%s_%g_%i_%s.json' % (self.outdir, kind, f, s,
+                                                       ch)
+                        save_clusters(kept, out)
+                        if self.res is not None:
+                            ClusterTable.from_clusters(kept, ch, self.res)\
+                                .to_tsv(out.replace('.json', '.tsv'))
+
+    def classify(self, chrom=None, fdr=0.05, cluster_size=3, n_threads=-1):
+        """Reference ``analysis.py:433-486``: significant pixels take the
+        condition of their largest alt-model mean and are re-clustered per
+        condition -> ``<cond>_<fdr>_<size>_<chrom>.json`` (+ ``.tsv``)."""
+        fdrs = list(fdr) if hasattr(fdr, '__len__') else [fdr]
+        sizes = list(cluster_size) if hasattr(cluster_size, '__len__') \
+            else [cluster_size]
+        for ch in self._chroms_for(chrom):
+            eprint('classifying differential interactions on chrom %s' % ch)
+            disp_idx = self.load_data('disp_idx', ch)
+            loop_idx = self.load_data('loop_idx', ch)
+            row = self.load_data('row', ch, idx=(disp_idx, loop_idx))
+            col = self.load_data('col', ch, idx=(disp_idx, loop_idx))
+            mu_hat_alt = self.load_data('mu_hat_alt', ch, idx=loop_idx)
+            for f in fdrs:
+                for s in sizes:
+                    infile = '%s/sig_%g_%i_%s.json' % (self.outdir, f, s, ch)
+                    if not os.path.isfile(infile):
+                        self.threshold(chrom=ch, fdr=f, cluster_size=s)
+                    sig = load_cluster_list(infile)
+                    per_class = classify_clusters(row, col, mu_hat_alt, sig)
+                    for i, cl in enumerate(per_class):
+                        out = '%s/%s_%g_%i_%s.json' % (
+                            self.outdir, self.design.columns[i], f, s, ch)
+                        save_clusters(cl, out)
+                        if self.res is not None:
+                            ClusterTable.from_clusters(cl, ch, self.res)\
+                                .to_tsv(out.replace('.json', '.tsv'))
+
+    def collect(self, fdr=0.05, cluster_size=3, n_threads=-1):
+        """Reference ``analysis.py:488-572``: every chromosome's insig
+        ("constitutive") and per-condition tables -> one sorted
+        ``results_<fdr>_<size>.tsv`` with a ``classification`` column."""
+        if self.res is None:
+            raise ValueError(
+                'the collect() step can only be run if the res kwarg was '
+                'passed during construction of the HiC3DeFDR object; please '
+                'run the classify() step instead or re-create the HiC3DeFDR '
+                'object (you do not need to re-run any other steps)')
+        eprint('collecting differential interactions')
+        fdrs = list(fdr) if hasattr(fdr, '__len__') else [fdr]
+        sizes = list(cluster_size) if hasattr(cluster_size, '__len__') \
+            else [cluster_size]
+        conds = list(self.design.columns)
+        for f in fdrs:
+            for s in sizes:
+                pattern = '%s/<class>_%g_%i_<chrom>.tsv' % (self.outdir, f, s)
+
+                def path(k, ch):
+                    return pattern.replace('<class>', k).replace('<chrom>', ch)
+                if not all(os.path.isfile(path('insig', ch))
+                           for ch in self.chroms):
+                    self.threshold(fdr=f, cluster_size=s)
+                if not all(os.path.isfile(path(c, ch)) for c in conds
+                           for ch in self.chroms):
+                    self.classify(fdr=f, cluster_size=s)
+                tables = []
+                for ch in self.chroms:
+                    tables.append(ClusterTable.read_tsv(path('insig', ch))
+                                  .with_classification('constitutive'))
+                    for c in conds:
+                        tables.append(ClusterTable.read_tsv(path(c, ch))
+                                      .with_classification(c))
+                ClusterTable.concat(tables).sorted().to_tsv(
+                    '%s/results_%g_%i.tsv' % (self.outdir, f, s))

@@ -19,9 +19,10 @@ ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 
-NATIVE_SRCS = ['h3d_api.hip']
+# (source, compiler): device TU through hipcc, host-only TUs through g++
+NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_calls.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
-           'h3d_prepare.h', 'h3d_prepare_api.h']
+           'h3d_prepare.h', 'h3d_prepare_api.h', 'h3d_errors.h']
 
 
 def _stale(target, deps):
@@ -48,16 +49,29 @@ def build_hosttest(force=False):
 
 
 def build_native(force=False):
-    os.makedirs(LIBDIR, exist_ok=True)
+    """Compiles each TU to an object (rebuilt only when it or a header is
+    newer), then links libh3d.so with hipcc."""
+    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
     out = os.path.join(LIBDIR, 'libh3d.so')
-    srcs = [os.path.join(CSRC, s) for s in NATIVE_SRCS]
-    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + \
-        [os.path.join(os.path.dirname(PKG), 'include', 'h3d.h')]
-    if force or _stale(out, deps):
-        _run([HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17',
-              '-shared', '-fPIC', '-munsafe-fp-atomics',
-              '-I', os.path.join(os.path.dirname(PKG), 'include'),
-              '-o', out] + srcs)
+    inc = os.path.join(os.path.dirname(PKG), 'include')
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(inc, 'h3d.h')]
+    objs = []
+    for src, cc in NATIVE_SRCS:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(LIBDIR, 'obj', src + '.o')
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            if cc == 'hipcc':
+                _run([HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17',
+                      '-fPIC', '-munsafe-fp-atomics', '-I', inc, '-c', '-o', o,
+                      s])
+            else:
+                _run(['g++', '-O2', '-std=c++17', '-fPIC', '-I', inc, '-c',
+                      '-o', o, s])
+    if force or _stale(out, objs):
+        _run([HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out]
+             + objs)
     return out
 
 

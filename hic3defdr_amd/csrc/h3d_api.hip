@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "h3d.h"
+#include "h3d_errors.h"
 #include "h3d_host.h"
 #include "h3d_kernels.h"
 #include "h3d_prepare.h"
@@ -20,17 +21,7 @@ using namespace h3d;
 
 namespace {
 
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
+using h3derr::fail;
 
 #define HIP_TRY(expr)                                                      \
   do {                                                                     \
@@ -270,7 +261,7 @@ extern "C" {
 
 int h3d_version(void) { return 1; }
 
-const char* h3d_last_error(void) { return g_err.c_str(); }
+const char* h3d_last_error(void) { return h3derr::last(); }
 
 int h3d_device_count(void) {
   int n = 0;

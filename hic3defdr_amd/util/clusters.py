@@ -1,10 +1,142 @@
-"""Sparse cluster JSON I/O (reference hic3defdr/util/clusters.py).
+"""Clusters of pixels (reference hic3defdr/util/clusters.py).
 
-Format: a JSON list of clusters, each a list of ``[i, j]`` pixel indices.
+Two forms:
+
+- the reference's: a list of sets of ``(i, j)`` tuples (``find_clusters``,
+  ``load_clusters``, ``save_clusters`` keep that API);
+- ``ClusterList``: the same clusters as arrays (pixel coordinates, a member
+  permutation and cluster start offsets), which the pipeline steps use so a
+  chromosome with millions of thresholded pixels never becomes millions of
+  Python tuples. Cluster numbering follows the reference's group order; within
+  a cluster, pixels keep their input order (the reference's JSON lists a
+  Python set in hash-table order, which carries no meaning -- only membership
+  is compared).
+
+Clustering itself is ``h3d_find_clusters`` in libh3d (host C++ restatement of
+the DirectedDisjointSet, clusters.py:15-97).
 """
 import json
 
 import numpy as np
+
+from hic3defdr_amd import _native
+
+
+class ClusterList(object):
+    """Cluster k = pixels ``(row[m], col[m])`` for
+    ``m in members[starts[k]:starts[k + 1]]``."""
+
+    def __init__(self, row, col, members, starts):
+        self.row = np.asarray(row, dtype=np.int64)
+        self.col = np.asarray(col, dtype=np.int64)
+        self.members = np.asarray(members, dtype=np.int64)
+        self.starts = np.asarray(starts, dtype=np.int64)
+
+    @classmethod
+    def empty(cls):
+        z = np.zeros(0, dtype=np.int64)
+        return cls(z, z, z, np.zeros(1, dtype=np.int64))
+
+    @classmethod
+    def from_labels(cls, row, col, labels, n_clusters):
+        """Group pixels by label (stable: input order inside a cluster)."""
+        members = np.argsort(labels, kind='stable')
+        counts = np.bincount(labels, minlength=n_clusters)
+        starts = np.zeros(n_clusters + 1, dtype=np.int64)
+        np.cumsum(counts, out=starts[1:])
+        return cls(row, col, members, starts)
+
+    @classmethod
+    def find(cls, row, col, connectivity=1):
+        """Clusters of the pixel list (row, col) in the reference's order
+        (``find_clusters`` on the COO of these pixels)."""
+        row = np.asarray(row, dtype=np.int64)
+        col = np.asarray(col, dtype=np.int64)
+        if len(row) == 0:
+            return cls.empty()
+        lab, nc = _native.cluster_labels(row, col, connectivity)
+        return cls.from_labels(row, col, lab, nc)
+
+    @classmethod
+    def from_sets(cls, clusters):
+        """From the reference form (list of iterables of (i, j))."""
+        rows, cols, sizes = [], [], []
+        for c in clusters:
+            c = list(c)
+            sizes.append(len(c))
+            for i, j in c:
+                rows.append(int(i))
+                cols.append(int(j))
+        starts = np.zeros(len(sizes) + 1, dtype=np.int64)
+        np.cumsum(sizes, out=starts[1:])
+        return cls(np.array(rows, dtype=np.int64),
+                   np.array(cols, dtype=np.int64),
+                   np.arange(len(rows), dtype=np.int64), starts)
+
+    def __len__(self):
+        return len(self.starts) - 1
+
+    def sizes(self):
+        return np.diff(self.starts)
+
+    def select(self, keep):
+        """Sub-list of the clusters where ``keep`` (bool per cluster)."""
+        keep = np.asarray(keep, dtype=bool)
+        sz = self.sizes()[keep]
+        idx = np.repeat(keep, self.sizes())
+        starts = np.zeros(len(sz) + 1, dtype=np.int64)
+        np.cumsum(sz, out=starts[1:])
+        return ClusterList(self.row, self.col, self.members[idx], starts)
+
+    def size_filter(self, cluster_size):
+        """thresholding.py:44-61: keep clusters with >= cluster_size pixels."""
+        return self.select(self.sizes() >= cluster_size)
+
+    def pixels(self):
+        """(row, col) of all member pixels, cluster by cluster."""
+        return self.row[self.members], self.col[self.members]
+
+    def bounds(self):
+        """Per-cluster (min row, max row, min col, max col)."""
+        if not len(self):
+            z = np.zeros(0, dtype=np.int64)
+            return z, z, z, z
+        r, c = self.pixels()
+        s = self.starts[:-1]
+        return (np.minimum.reduceat(r, s), np.maximum.reduceat(r, s),
+                np.minimum.reduceat(c, s), np.maximum.reduceat(c, s))
+
+    def texts(self):
+        """Per-cluster text ``[[i, j], [i, j]]`` as a list of str."""
+        if not len(self):
+            return []
+        buf, ends = _native.format_clusters(self.row, self.col, self.members,
+                                            self.starts)
+        b = np.concatenate([[0], ends])
+        s = buf.decode('ascii')
+        return [s[b[k]:b[k + 1]] for k in range(len(self))]
+
+    def json_text(self):
+        """save_clusters text (clusters.py:129-130, json.dump defaults)."""
+        if not len(self):
+            return '[]'
+        buf, _ = _native.format_clusters(self.row, self.col, self.members,
+                                         self.starts)
+        # clusters are adjacent "[...]" blocks: join them with ", "
+        return '[' + buf.decode('ascii').replace(']][[', ']], [[') + ']'
+
+    def to_sets(self):
+        r, c = self.pixels()
+        return [set(zip(r[a:b].tolist(), c[a:b].tolist()))
+                for a, b in zip(self.starts[:-1], self.starts[1:])]
+
+
+def find_clusters(sig_points, connectivity=1):
+    """Reference ``clusters.py:73-97``: clusters of the True entries of a
+    boolean matrix (scipy sparse or dense), as a list of sets of tuples."""
+    import scipy.sparse as sparse
+    m = sparse.coo_matrix(sig_points)
+    return ClusterList.find(m.row, m.col, connectivity).to_sets()
 
 
 def load_clusters(infile):
@@ -14,11 +146,36 @@ def load_clusters(infile):
                 json.load(handle)]
 
 
+def load_cluster_list(infile):
+    """A cluster JSON as a ``ClusterList`` (file order kept)."""
+    with open(infile, 'r') as handle:
+        data = json.load(handle)
+    return ClusterList.from_sets(data)
+
+
 def save_clusters(clusters, outfile):
-    """Reference ``clusters.py:116-136``."""
+    """Reference ``clusters.py:116-136`` (list of sets or a ClusterList)."""
     with open(outfile, 'w') as handle:
-        json.dump([[[int(i), int(j)] for i, j in cluster]
-                   for cluster in clusters], handle)
+        if isinstance(clusters, ClusterList):
+            handle.write(clusters.json_text())
+        else:
+            json.dump([[[int(i), int(j)] for i, j in cluster]
+                       for cluster in clusters], handle)
+
+
+def cluster_to_loop_id(cluster, chrom, resolution):
+    """Reference ``clusters.py:300-330``: "chr:start-end_chr:start-end"."""
+    x, y = zip(*cluster)
+    return '%s:%s-%s_%s:%s-%s' % (chrom, min(x) * resolution,
+                                  (max(x) + 1) * resolution, chrom,
+                                  min(y) * resolution,
+                                  (max(y) + 1) * resolution)
+
+
+def cluster_from_string(cluster_string):
+    """Reference ``clusters.py:333-360``."""
+    return json.loads(cluster_string.replace('(', '[').replace('{', '[')
+                      .replace(')', ']').replace('}', ']'))
 
 
 def pixel_membership(row, col, clusters_lists, n_bins=None):
@@ -29,7 +186,16 @@ def pixel_membership(row, col, clusters_lists, n_bins=None):
     if not pixels or len(row) == 0:
         return np.zeros(len(row), dtype=bool)
     pix = np.array(sorted(pixels), dtype=np.int64)
-    base = int(max(pix.max(), int(np.max(row)), int(np.max(col)))) + 1
-    keys = np.asarray(row, dtype=np.int64) * base + np.asarray(col, np.int64)
-    pk = pix[:, 0] * base + pix[:, 1]
-    return np.isin(keys, pk)
+    return pixel_in(row, col, pix[:, 0], pix[:, 1])
+
+
+def pixel_in(row, col, prow, pcol):
+    """(row[k], col[k]) in the pixel set {(prow, pcol)} (vectorised)."""
+    row = np.asarray(row, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    if len(row) == 0 or len(prow) == 0:
+        return np.zeros(len(row), dtype=bool)
+    prow = np.asarray(prow, dtype=np.int64)
+    pcol = np.asarray(pcol, dtype=np.int64)
+    base = int(max(pcol.max(), col.max())) + 1
+    return np.isin(row * base + col, prow * base + pcol)

@@ -16,6 +16,10 @@
  *   h3d_lrt                <- util/lrt.py:7-50 (+ analysis/analysis.py:272-278)
  *   h3d_bh                 <- analysis/analysis.py:286-303 (lib5c
  *                              adjust_pvalues = BH)
+ *   h3d_find_clusters      <- util/clusters.py:73-97 find_clusters (threshold /
+ *                              classify, analysis.py:366-486)
+ *   h3d_format_clusters    <- util/clusters.py:129-130 save_clusters text,
+ *                              util/cluster_table.py:67 "cluster" column
  *
  * Conventions: 0 on success, a negative H3D_E* code otherwise (the message is
  * in h3d_last_error(), thread-local). Host buffers are C-contiguous and owned
@@ -138,6 +142,25 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 
 /* Benjamini-Hochberg q-values over the finite p-values (NaN elsewhere). */
 int h3d_bh(const double* p, int64_t n, double* q);
+
+/* ---- threshold / classify / collect (host) ------------------------------ */
+
+/* Clusters of a pixel list (clusters.py:73-97 find_clusters with its
+ * DirectedDisjointSet, :15-70): connectivity 1 = 4-neighbour cross, 2 = the
+ * 8-neighbourhood (scipy generate_binary_structure(2, connectivity)).
+ * label[i] = cluster of pixel i, numbered in the order of the reference's
+ * get_groups() list; *n_clusters = number of clusters. Host code. */
+int h3d_find_clusters(const int64_t* row, const int64_t* col, int64_t n,
+                      int connectivity, int64_t* label, int64_t* n_clusters);
+
+/* "[[i, j], [i, j], ...]" text of each cluster (clusters.py:129-130 JSON,
+ * cluster_table.py:67 TSV "cluster" column): cluster k is the pixels
+ * order[starts[k] .. starts[k+1]). Concatenated into buf (cap bytes; NULL to
+ * size), ends[k] = end offset of cluster k (optional), *len = total bytes. */
+int h3d_format_clusters(const int64_t* row, const int64_t* col,
+                        const int64_t* order, const int64_t* starts,
+                        int64_t n_clusters, char* buf, int64_t cap,
+                        int64_t* ends, int64_t* len);
 
 /* ---- measurement -------------------------------------------------------- */
 

@@ -252,8 +252,108 @@ def unit_scaling():
     np.savez_compressed(os.path.join(HERE, 'unit_scaling.npz'), **out)
 
 
+CALL_FDRS = [0.05, 0.2]
+CALL_SIZES = [1, 3]
+
+
+def run_calls(name):
+    """threshold -> classify -> collect on the committed e2e inputs
+    (analysis.py:366-572). Every JSON / TSV the reference writes is stored
+    verbatim (as bytes) in calls_<name>.npz.
+
+    Patch (recorded as meta_load_data_patch): without loop_patterns the
+    reference's load_data('loop_idx') calls the non-existent np.load_data
+    (core.py:105); the generator routes it to the intended HiC3DeFDR.load_data
+    so the no-loop dataset can be thresholded too."""
+    sizes, dmax, npc, seed, loops = E2E[name]
+    base = os.path.join(HERE, 'data', name)
+    g = np.load(os.path.join(HERE, 'e2e_%s.npz' % name))
+    reps = [str(r) for r in g['meta_reps']]
+    conds = [str(c) for c in g['meta_conds']]
+    chroms = [str(c) for c in g['meta_chroms']]
+    design = pd.DataFrame(g['meta_design'].astype(bool), index=reps,
+                          columns=conds)
+    outdir = os.path.join('/tmp', 'h3golden_calls_' + name)
+    shutil.rmtree(outdir, ignore_errors=True)
+    lp = {c: os.path.join(base, 'clusters', '%s_<chrom>.json' % c)
+          for c in conds} if loops else None
+    h = HiC3DeFDR(raw_npz_patterns=[os.path.join(base, r, '<chrom>_raw.npz')
+                                    for r in reps],
+                  bias_patterns=[os.path.join(base, r, '<chrom>_kr.bias')
+                                 for r in reps],
+                  chroms=chroms, design=design, outdir=outdir,
+                  dist_thresh_max=dmax, loop_patterns=lp, res=10000)
+    np.load_data = lambda nm, ch: h.load_data(nm, ch)
+    h.run_to_qvalues(n_threads=0, verbose=False)
+    for c in chroms:  # same q-values as the e2e golden
+        q = np.load(os.path.join(outdir, 'qvalues_%s.npy' % c))
+        assert np.array_equal(q, g['qvalues__%s' % c], equal_nan=True)
+    h.collect(fdr=CALL_FDRS, cluster_size=CALL_SIZES, n_threads=0)
+    out = {'meta_fdrs': np.array(CALL_FDRS), 'meta_sizes': np.array(CALL_SIZES),
+           'meta_res': np.array(10000),
+           'meta_load_data_patch': np.array(not loops)}
+    files = sorted(f for f in os.listdir(outdir)
+                   if f.endswith('.json') or f.endswith('.tsv'))
+    for f in files:
+        with open(os.path.join(outdir, f), 'rb') as fh:
+            out['file__' + f] = np.frombuffer(fh.read(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, 'calls_%s.npz' % name), **out)
+    print(name, 'call files', len(files))
+
+
+def unit_clusters():
+    """find_clusters (clusters.py:73-97) on random pixel sets, connectivity 1
+    and 2, plus classify (classification.py:7-49). Clusters are stored in the
+    reference's group order, each cluster's pixels sorted."""
+    from hic3defdr.util.clusters import find_clusters
+    from hic3defdr.util.classification import classify
+    import scipy.sparse as sp
+    rng = np.random.default_rng(15)
+    out = {}
+    for t in range(8):
+        n = int(rng.integers(5, 60))
+        dens = float(rng.uniform(0.05, 0.6))
+        m = rng.random((n, n)) < dens
+        if t % 2:
+            m = np.triu(m)
+        r, c = np.nonzero(m)
+        perm = rng.permutation(r.size) if t >= 4 else np.arange(r.size)
+        r, c = r[perm], c[perm]
+        out['cl%d_row' % t] = r
+        out['cl%d_col' % t] = c
+        for conn in (1, 2):
+            coo = sp.coo_matrix((np.ones(r.size, dtype=bool), (r, c)),
+                                shape=(n, n))
+            groups = find_clusters(coo, connectivity=conn)
+            lab = np.full(r.size, -1)
+            key = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(r, c))}
+            for gi, grp in enumerate(groups):
+                for p in grp:
+                    lab[key[(int(p[0]), int(p[1]))]] = gi
+            out['cl%d_label_c%d' % (t, conn)] = lab
+        # classify: value rows parallel to (r, c), 3 classes, some ties
+        val = rng.integers(0, 4, (r.size, 3)).astype(float)
+        sig = [g for g in find_clusters(
+            sp.coo_matrix((np.ones(r.size, dtype=bool), (r, c)),
+                          shape=(n, n))) if len(g) >= 2]
+        cls = classify(r, c, val, sig)
+        out['cl%d_val' % t] = val
+        out['cl%d_sig' % t] = json.dumps(
+            [sorted([int(a), int(b)] for a, b in g) for g in sig])
+        out['cl%d_classify' % t] = json.dumps(
+            [[sorted([int(a), int(b)] for a, b in g) for g in k]
+             for k in cls])
+    np.savez_compressed(os.path.join(HERE, 'unit_clusters.npz'), **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling']
+    which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling',
+                             'calls', 'clusters']
+    if 'calls' in which:
+        for name in E2E:
+            run_calls(name)
+    if 'clusters' in which:
+        unit_clusters()
     if 'e2e' in which:
         for name in E2E:
             run_e2e(name)

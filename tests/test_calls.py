@@ -1,0 +1,194 @@
+"""threshold -> classify -> collect (reference analysis.py:366-572) against the
+reference's own outputs (tests/golden/calls_<name>.npz, unit_clusters.npz,
+written by tests/golden/make_golden.py).
+
+These steps are host code in libh3d (h3d_find_clusters / h3d_format_clusters)
+and run here on the CPU: the outdir is filled with the reference's arrays
+(row, col, disp_idx, loop_idx, mu_hat_alt, qvalues), so the calls are compared
+on identical q-values. The GPU-computed q-values feed the same steps in
+tests/test_gpu_e2e.py.
+
+Parity bar: every cluster (sig, insig, per condition) has the same pixel set,
+and the clusters come in the same order (the reference's group order); every
+TSV has the same rows in the same order, byte for byte except the "cluster"
+column, whose pixel order is a CPython set's hash-table order in the reference
+(compared as a set).
+"""
+import json
+import os
+import shutil
+import tempfile
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import e2e_inputs, golden
+
+from hic3defdr_amd import _native
+from hic3defdr_amd.util import clusters as ucl
+from hic3defdr_amd.util.classification import classify
+from hic3defdr_amd.util.cluster_table import (clusters_to_table,
+                                              load_cluster_table,
+                                              sort_cluster_table)
+
+
+def _pixsets(text):
+    return [frozenset(map(tuple, c)) for c in json.loads(text)]
+
+
+def _cluster_set(text):
+    return frozenset(map(tuple, json.loads(text)))
+
+
+def test_find_clusters_matches_reference_order():
+    g = golden('unit_clusters.npz')
+    for t in range(8):
+        r, c = g['cl%d_row' % t], g['cl%d_col' % t]
+        for conn in (1, 2):
+            lab, nc = _native.cluster_labels(r, c, conn)
+            ref = g['cl%d_label_c%d' % (t, conn)]
+            np.testing.assert_array_equal(lab, ref)
+            assert nc == ref.max() + 1
+
+
+def test_classify_matches_reference():
+    g = golden('unit_clusters.npz')
+    for t in range(8):
+        r, c = g['cl%d_row' % t], g['cl%d_col' % t]
+        sig = [set(map(tuple, s)) for s in json.loads(str(g['cl%d_sig' % t]))]
+        got = classify(r, c, g['cl%d_val' % t], sig)
+        ref = json.loads(str(g['cl%d_classify' % t]))
+        assert len(got) == len(ref)
+        for k in range(len(ref)):
+            assert [frozenset(x) for x in got[k]] == \
+                [frozenset(map(tuple, x)) for x in ref[k]]
+
+
+def test_find_clusters_api_and_edge_cases():
+    import scipy.sparse as sp
+    # reference doctest shapes: two separate blocks, diagonal contact only
+    m = np.zeros((6, 6), dtype=bool)
+    m[1, 1] = m[1, 2] = m[4, 4] = m[3, 4] = m[5, 5] = True
+    got = ucl.find_clusters(sp.coo_matrix(m))
+    assert [frozenset(x) for x in got] == [
+        frozenset({(1, 1), (1, 2)}), frozenset({(3, 4), (4, 4)}),
+        frozenset({(5, 5)})]
+    # 8-connectivity joins the diagonal neighbour
+    got = ucl.find_clusters(sp.coo_matrix(m), connectivity=2)
+    assert [frozenset(x) for x in got] == [
+        frozenset({(1, 1), (1, 2)}), frozenset({(3, 4), (4, 4), (5, 5)})]
+    assert ucl.find_clusters(sp.coo_matrix((4, 4), dtype=bool)) == []
+    # duplicate COO entries collapse into one pixel
+    lab, nc = _native.cluster_labels([2, 2, 3], [3, 3, 3])
+    assert nc == 1 and list(lab) == [0, 0, 0]
+    with pytest.raises(_native.H3DError):
+        _native.cluster_labels([-1], [0])
+
+
+def test_cluster_table_doctests():
+    # cluster_table.py:59-70 and :104-126
+    df = clusters_to_table([[(1, 2), (1, 1)], [(4, 4), (3, 4)]], 'chrX',
+                           10000)
+    row = df.iloc[0]
+    assert df.index[0] == 'chrX:10000-20000_chrX:10000-30000'
+    assert (row['us_start'], row['us_end'], row['ds_start'],
+            row['ds_end'], row['cluster_size']) == (10000, 20000, 10000,
+                                                    30000, 2)
+    assert sorted(row['cluster']) == [[1, 1], [1, 2]]
+    cl = [[(4, 4), (3, 4)], [(1, 2), (1, 1)]]
+    dfs = [clusters_to_table(cl, c, 10000)
+           for c in ('chrX', 'chr11', 'chr2', 'chr1')]
+    idx = list(sort_cluster_table(pd.concat(dfs, axis=0)).index)
+    assert idx == [
+        'chr1:10000-20000_chr1:10000-30000', 'chr1:30000-50000_chr1:40000-50000',
+        'chr2:10000-20000_chr2:10000-30000', 'chr2:30000-50000_chr2:40000-50000',
+        'chr11:10000-20000_chr11:10000-30000',
+        'chr11:30000-50000_chr11:40000-50000',
+        'chrX:10000-20000_chrX:10000-30000', 'chrX:30000-50000_chrX:40000-50000']
+    assert ucl.cluster_to_loop_id([(4, 5), (3, 4), (3, 5), (3, 6)], 'chrX',
+                                  10000) == 'chrX:30000-50000_chrX:40000-70000'
+    assert ucl.cluster_from_string('[(4, 5), (3, 4)]') == [[4, 5], [3, 4]]
+
+
+def fill_outdir_from_golden(name, outdir):
+    """The reference's outdir arrays for the e2e dataset -> outdir; returns
+    a HiC3DeFDR bound to it (res 10 kb, as the goldens)."""
+    from hic3defdr_amd import HiC3DeFDR
+    g, kw = e2e_inputs(name)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir,
+                  dist_thresh_max=kw['dist_thresh_max'],
+                  loop_patterns=kw['loop_patterns'], res=10000)
+    for c in kw['chroms']:
+        for st in ('row', 'col', 'disp_idx', 'loop_idx', 'mu_hat_alt',
+                   'qvalues'):
+            k = '%s__%s' % (st, c)
+            if k in g.files:
+                np.save(os.path.join(outdir, '%s_%s.npy' % (st, c)), g[k])
+    return h
+
+
+def assert_calls_match(outdir, name):
+    """Every JSON / TSV of the reference's calls vs the files in outdir."""
+    ref = golden('calls_%s.npz' % name)
+    files = [k[len('file__'):] for k in ref.files if k.startswith('file__')]
+    assert files
+    for fn in files:
+        want = bytes(ref['file__' + fn]).decode()
+        path = os.path.join(outdir, fn)
+        assert os.path.isfile(path), fn
+        got = open(path).read()
+        if fn.endswith('.json'):
+            assert _pixsets(got) == _pixsets(want), fn
+            continue
+        gl, wl = got.split('\n'), want.split('\n')
+        assert len(gl) == len(wl), fn
+        assert gl[0] == wl[0], fn
+        for a, b in zip(gl[1:], wl[1:]):
+            fa, fb = a.split('\t'), b.split('\t')
+            assert len(fa) == len(fb), (fn, a, b)
+            ci = wl[0].split('\t').index('cluster') if fb != [''] else None
+            if ci is None:
+                assert a == b, fn
+                continue
+            assert fa[:ci] == fb[:ci] and fa[ci + 1:] == fb[ci + 1:], (fn, a, b)
+            assert _cluster_set(fa[ci]) == _cluster_set(fb[ci]), (fn, a, b)
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+def test_calls_on_reference_qvalues(name):
+    outdir = tempfile.mkdtemp(prefix='h3d_calls_')
+    try:
+        h = fill_outdir_from_golden(name, outdir)
+        ref = golden('calls_%s.npz' % name)
+        fdrs = [float(x) for x in ref['meta_fdrs']]
+        sizes = [int(x) for x in ref['meta_sizes']]
+        h.collect(fdr=fdrs, cluster_size=sizes)
+        assert_calls_match(outdir, name)
+        # the results table reads back with the reference's loader
+        df = load_cluster_table(os.path.join(outdir, 'results_%g_%i.tsv'
+                                             % (fdrs[0], sizes[0])))
+        assert set(df['classification']) <= {'constitutive'} | \
+            set(h.design.columns)
+        assert (df['cluster_size'] == df['cluster'].map(len)).all()
+    finally:
+        shutil.rmtree(outdir, ignore_errors=True)
+
+
+def test_collect_needs_res():
+    from hic3defdr_amd import HiC3DeFDR
+    outdir = tempfile.mkdtemp(prefix='h3d_calls_')
+    try:
+        _, kw = e2e_inputs('small2')
+        design = pd.DataFrame(kw['design'], index=kw['reps'],
+                              columns=kw['conds'])
+        h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                      bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                      design=design, outdir=outdir)
+        with pytest.raises(ValueError):
+            h.collect()
+    finally:
+        shutil.rmtree(outdir, ignore_errors=True)

@@ -9,7 +9,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from conftest import e2e_inputs, rel_err
+from conftest import e2e_inputs, golden, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -66,5 +66,12 @@ def test_run_to_qvalues_matches_reference(name):
         assert off[-1] == len(q_all)
         r, cc, v = h2.load_data('qvalues', kw['chroms'][0], coo=True)
         assert len(r) == len(cc) == len(v)
+        # downstream calls on the GPU q-values: same clusters, same tables
+        # as the reference (threshold -> classify -> collect)
+        from test_calls import assert_calls_match
+        ref = golden('calls_%s.npz' % name)
+        h2.collect(fdr=[float(x) for x in ref['meta_fdrs']],
+                   cluster_size=[int(x) for x in ref['meta_sizes']])
+        assert_calls_match(outdir, name)
     finally:
         shutil.rmtree(outdir, ignore_errors=True)
