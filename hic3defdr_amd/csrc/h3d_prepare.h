@@ -196,7 +196,17 @@ __global__ void k_mor_keys(const double* __restrict__ balanced,
     const double gm = exp(s / R) - 1;
     for (int r = 0; r < R; ++r)
       keys[(int64_t)r * n + k] = ok ? balanced[i * R + r] / gm : INFINITY;
-    if (ok) atomicAdd(&valid_per_bin[bin[k]], 1);
+    // valid rows per bin: bins are sorted along k, so a wave spans one or
+    // two bins -- one atomic per (wave, bin) instead of one per row
+    const int b = bin[k];
+    unsigned long long pend = __ballot(ok);
+    while (pend) {
+      const int leader = __ffsll((long long)pend) - 1;
+      const int bl = __shfl(b, leader, 64);
+      const unsigned long long same = __ballot(ok && b == bl) & pend;
+      if ((int)(threadIdx.x & 63) == leader) atomicAdd(&valid_per_bin[bl], (int)__popcll(same));
+      pend &= ~same;
+    }
   }
 }
 
@@ -224,12 +234,22 @@ __global__ void k_mor_median(const double* __restrict__ sorted_keys,
 __global__ void k_bin_dist_sum(const int32_t* __restrict__ dist_sorted,
                                const int64_t* __restrict__ bin_start,
                                int n_bins, double* __restrict__ d_per_bin) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // one workgroup per bin; integer sum, so the reduction order is free
+  __shared__ long long part[16];
+  const int b = blockIdx.x;
   if (b >= n_bins) return;
   long long s = 0;
-  for (int64_t k = bin_start[b]; k < bin_start[b + 1]; ++k) s += dist_sorted[k];
-  const int64_t cnt = bin_start[b + 1] - bin_start[b];
-  d_per_bin[b] = cnt ? (double)s / (double)cnt : NAN;
+  for (int64_t k = bin_start[b] + threadIdx.x; k < bin_start[b + 1]; k += blockDim.x)
+    s += dist_sorted[k];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    const int64_t cnt = bin_start[b + 1] - bin_start[b];
+    d_per_bin[b] = cnt ? (double)t / (double)cnt : NAN;
+  }
 }
 
 // sf[i, r] = interp1d(d_per_bin, s_per_bin[:, r], extrapolate)(dist[i]) over

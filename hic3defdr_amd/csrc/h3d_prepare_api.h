@@ -231,7 +231,7 @@ int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
   hipLaunchKernelGGL(k_mor_median, dim3((nb * R + 255) / 256), dim3(256), 0, s, d_keys_s,
                      d_bstart, d_valid, nb, n, R, d_spb);
   if (n_bins > 0) {
-    hipLaunchKernelGGL(k_bin_dist_sum, dim3((nb + 255) / 256), dim3(256), 0, s, d_dist_s,
+    hipLaunchKernelGGL(k_bin_dist_sum, dim3(nb), dim3(256), 0, s, d_dist_s,
                        d_bstart, nb, d_dpb);
     std::vector<double> dpb(nb), spb((size_t)nb * R);
     HIP_TRY(hipMemcpyAsync(dpb.data(), d_dpb, nb * 8, hipMemcpyDeviceToHost, s));

@@ -644,12 +644,71 @@ H3D_HD double find_inverse_gamma(double a, double p, double q, double lga) {
   return result;
 }
 
+// P(a, xe + h) - P(a, xe) and P'(xe + h) / P'(xe) from P'(xe) alone, for a
+// step h: P'(x) = x^(a-1) e^-x / Gamma(a), so
+//   P'(xe + s) / P'(xe) = exp(g(s)),  g(s) = (a-1) ln(1 + s/xe) - s,
+// and exp(g) = sum e_k s^k by the power-series exponential recurrence
+// e_k = (1/k) sum_j j g_j e_(k-j) on g's Taylor coefficients
+// g_j = (a-1) (-1)^(j+1) / (j xe^j) (- 1 for j = 1). K = 12 terms, fixed
+// length (no lane divergence). Used inside the window igam_taylor_ok, where
+// the dropped terms are below (|g_1 h|)^13 / 13! and |a-1| (h/xe)^13 / 13,
+// i.e. < 2e-15 x/h of the increment -- the root it leads to moves < 1e-16
+// relative.
+constexpr int kTaylorK = 12;
+
+H3D_HD bool igam_taylor_ok(double a, double xe, double h) {
+  const double u = h / xe;
+  return xe > 0.0 && fabs(u) <= 0.05 &&
+         fabs(((a - 1.0) / xe - 1.0) * h) <= 0.4 &&
+         fabs(a - 1.0) * u * u <= 0.25;
+}
+
+H3D_HD void igam_step_taylor(double a, double xe, double h, double* dint,
+                             double* ratio) {
+  constexpr int K = kTaylorK;
+  constexpr double inv[K + 2] = {0.0, 1.0, 1.0 / 2, 1.0 / 3, 1.0 / 4,
+                                 1.0 / 5, 1.0 / 6, 1.0 / 7, 1.0 / 8, 1.0 / 9,
+                                 1.0 / 10, 1.0 / 11, 1.0 / 12, 1.0 / 13};
+  const double b = a - 1.0;
+  // work in s = h t (t in [0, 1]): c_j = g_j h^j, so every coefficient is
+  // O(rho^j) and exp(g(h t)) = sum E_k t^k with E_k = e_k h^k
+  const double u = h / xe;
+  double jc[K + 1];  // j * c_j
+  double pw = u;
+  for (int j = 1; j <= K; ++j) {
+    jc[j] = (j & 1) ? b * pw : -b * pw;
+    pw *= u;
+  }
+  jc[1] -= h;
+  double E[K + 1];
+  E[0] = 1.0;
+  for (int k = 1; k <= K; ++k) {
+    double acc = 0.0;
+    for (int j = 1; j <= k; ++j) acc += jc[j] * E[k - j];
+    E[k] = acc * inv[k];
+  }
+  // integral_0^h = h sum E_k / (k+1); exp(g(h)) = sum E_k
+  double in = 0.0, ex = 0.0;
+  for (int k = K; k >= 0; --k) {
+    in += E[k] * inv[k + 1];
+    ex += E[k];
+  }
+  *dint = in * h;
+  *ratio = ex;
+}
+
 // Inverse incomplete gamma on either tail: solves P(a, x) = t (upper=false)
 // or Q(a, x) = t (upper=true), t in (0, 1), given lga = lgam(a). As scipy's
 // igami/igamci it always works on the tail that is <= 0.9 and refines the
-// DiDonato & Morris guess with Halley steps (f''/f' = (a-1)/x - 1); each step
-// costs one igam_pq. It stops once a step moved x by <= 1e-6 relative: Halley
-// converges cubically, so the error left is ~1e-18 (scipy always takes 3).
+// DiDonato & Morris guess with Halley steps (f''/f' = (a-1)/x - 1). It stops
+// once a step moved x by <= 1e-6 relative: Halley converges cubically, so the
+// error left is ~1e-18 (scipy always takes 3).
+// Residual evaluation: a full igam_pq where x moved far from the last full
+// evaluation xe; otherwise the residual is continued from xe by the Taylor
+// increment of P (igam_step_taylor), which is exact to ~1e-17 of the step and
+// costs ~40 flops instead of a series / continued fraction. A good guess
+// (~1e-4 relative) thus takes ONE incomplete-gamma evaluation: the confirming
+// Halley step runs on the continuation.
 H3D_HD double igam_inv(double a, double t, bool upper, double lga,
                        double guess = -1.0) {
   H3D_STAT(inv, 1);
@@ -661,12 +720,30 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
   double x = (guess > 0.0) ? guess
                            : upper ? find_inverse_gamma(a, 1.0 - t, t, lga)
                                    : find_inverse_gamma(a, t, 1.0 - t, lga);
+  // last full evaluation: point, residual F = tail(x) - t, slope P'(x)
+  double xe = -1.0, Fe = 0.0, dPe = 0.0;
   for (int i = 0; i < 8; ++i) {
     H3D_STAT(halley, 1);
-    double P, Q, fac;
-    igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
-    if (fac == 0.0) return x;
-    const double f_fp = upper ? (Q - t) * x / (-fac) : (P - t) * x / fac;
+    double F, dP;
+    const double h = x - xe;
+    if (igam_taylor_ok(a, xe, h)) {
+      double dint, ratio;
+      igam_step_taylor(a, xe, h, &dint, &ratio);
+      const double dPint = dPe * dint;  // P(x) - P(xe)
+      F = upper ? Fe - dPint : Fe + dPint;
+      dP = dPe * ratio;
+    } else {
+      double P, Q, fac;
+      igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
+      if (fac == 0.0) return x;
+      F = (upper ? Q : P) - t;
+      dP = fac / x;
+      xe = x;
+      Fe = F;
+      dPe = dP;
+    }
+    // Newton ratio f / f' (f' = -P' on the upper tail), Halley correction
+    const double f_fp = upper ? -F / dP : F / dP;
     const double fpp_fp = -1.0 + (a - 1) / x;
     double xn = is_inf(fpp_fp) ? x - f_fp
                                : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
