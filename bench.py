@@ -149,8 +149,7 @@ def main():
             dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                         t_dist.data_ptr(), n, R, cond, C, D,
                                         reduce=reduce)
-            tab = np.stack([_native.disp_table(dpd[:, c]) for c in range(C)],
-                           axis=1)
+            tab = _native.disp_tables(dpd)
             ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
                         tab, n, R, cond, t_p.data_ptr(), t_llr.data_ptr(),
                         t_mu0.data_ptr(), t_mu1.data_ptr(), t_disp.data_ptr())

@@ -286,6 +286,29 @@ def disp_table(disp_per_dist_col, weighted=True, frac=None,
     return out
 
 
+_table_pool = None
+
+
+def disp_tables(disp_per_dist, weighted=True, frac=None, auto_frac_factor=15.):
+    """disp_table for every column of ``disp_per_dist`` (D, C), the
+    conditions smoothed concurrently (ctypes drops the GIL inside libh3d, and
+    the smoother is a serial few-hundred-point computation per condition)."""
+    global _table_pool
+    d = np.asarray(disp_per_dist, dtype=np.float64)
+    C = d.shape[1]
+    def one(c):
+        return disp_table(d[:, c], weighted=weighted, frac=frac,
+                          auto_frac_factor=auto_frac_factor)
+    if C == 1:
+        return one(0)[:, None]
+    with _lock:
+        if _table_pool is None:
+            import concurrent.futures
+            _table_pool = concurrent.futures.ThreadPoolExecutor(
+                max_workers=8, thread_name_prefix='h3d_lowess')
+    return np.stack(list(_table_pool.map(one, range(C))), axis=1)
+
+
 def bh(pvalues):
     lib = load_library()
     p = _c(pvalues, np.float64)

@@ -143,11 +143,12 @@ class AnalyzingHiC3DeFDR(object):
                 'place for cml/mme (dispersion.py:76,129) and raises; the GPU '
                 'path implements %s' % (estimator, NATIVE_ESTIMATORS))
         disp = np.zeros((len(raw), C))
+        eprint('  fitting distance vs dispersion relationship')
+        tables = _native.disp_tables(disp_per_dist, weighted=weighted_lowess,
+                                     frac=frac,
+                                     auto_frac_factor=auto_frac_factor)
         for c, cond in enumerate(self.design.columns):
-            eprint('  fitting distance vs dispersion relationship')
-            table = _native.disp_table(disp_per_dist[:, c],
-                                       weighted=weighted_lowess, frac=frac,
-                                       auto_frac_factor=auto_frac_factor)
+            table = tables[:, c]
             fn = DispFn(table, disp_per_dist[:, c], weighted=weighted_lowess)
             disp[:, c] = table[dist]
             self.save_disp_fn(cond, fn)

@@ -59,10 +59,14 @@ struct h3d_ctx {
   PrepUnion prep;
   // [equalize, nll] pixel-replicates processed by disp_work (measurement)
   unsigned long long* work_count = nullptr;
+  // pinned host word the disp loop polls (active work items), kept for the
+  // ctx's lifetime (a per-call hipHostFree would synchronise the device)
+  int32_t* h_meta = nullptr;
   // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
-  // disp_work register budget (1, 3, 4); H3D_DISP_SORT = 0 (distance) or
+  // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
   // 1 (distance, total count)
-  int disp_w = 4;     // measured best (r01 sweep: 1 / 3 / 4 -> 52.5 / 53.5 / 50.4 ms)
+  int disp_w = 4;  // measured best (sweep at 7413b12, equalize ms/step for
+                   // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
   int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
 };
 
@@ -206,6 +210,11 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
         hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
                            ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
                            n_rep, st, seg_flags, list, meta, partial);
+      } else if (ctx->disp_w == 2) {
+        auto k = k_disp_work<M, 2, kEqualize>;
+        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
+                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
+                           n_rep, st, seg_flags, list, meta, partial);
       } else {
         done = false;
       }
@@ -323,6 +332,7 @@ void h3d_close(h3d_ctx* ctx) {
     if (kv.second.first) (void)hipFree(kv.second.first);
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->work_count) (void)hipFree(ctx->work_count);
+  if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -407,22 +417,40 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     int end_bit = 1;
     while ((1 << end_bit) <= D) ++end_bit;
     size_t tmp_bytes = 0;
-    if (ctx->disp_sort == 1) {
-      // (distance, total count) keys: same segments, less lane divergence
-      uint64_t* keys = (uint64_t*)scratch(ctx, "dkeys", n * 8);
-      uint64_t* keys_s = (uint64_t*)scratch(ctx, "dkeys_s", n * 8);
+    if (ctx->disp_sort == 1 && end_bit <= 16) {
+      // (distance, total count) keys: same segments, less lane divergence;
+      // 32-bit keys (16 count bits) whenever the distance fits 16 bits
+      constexpr int cbits = 16;
+      uint32_t* keys = (uint32_t*)scratch(ctx, "dkeys", n * 4);
+      uint32_t* keys_s = (uint32_t*)scratch(ctx, "dkeys_s", n * 4);
       if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
-      hipLaunchKernelGGL(k_dist_count_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                         d_dist, d_raw, n, R, keys);
+      hipLaunchKernelGGL(k_dist_count_keys<uint32_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
+                         0, s, d_dist, d_raw, n, R, cbits, keys);
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s,
                                                  idx_in, idx_out, (int)n, 0,
-                                                 32 + end_bit, s));
+                                                 cbits + end_bit, s));
       void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
       if (!tmp) return fail(H3D_ENOMEM, "sort temp");
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_s, idx_in,
-                                                 idx_out, (int)n, 0, 32 + end_bit, s));
-      hipLaunchKernelGGL(k_key_dist, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                         keys_s, n, dist_s);
+                                                 idx_out, (int)n, 0, cbits + end_bit, s));
+      hipLaunchKernelGGL(k_key_dist<uint32_t>, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         keys_s, n, cbits, dist_s);
+    } else if (ctx->disp_sort == 1) {
+      constexpr int cbits = 32;
+      uint64_t* keys = (uint64_t*)scratch(ctx, "dkeys", n * 8);
+      uint64_t* keys_s = (uint64_t*)scratch(ctx, "dkeys_s", n * 8);
+      if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
+      hipLaunchKernelGGL(k_dist_count_keys<uint64_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
+                         0, s, d_dist, d_raw, n, R, cbits, keys);
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s,
+                                                 idx_in, idx_out, (int)n, 0,
+                                                 cbits + end_bit, s));
+      void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+      if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_s, idx_in,
+                                                 idx_out, (int)n, 0, cbits + end_bit, s));
+      hipLaunchKernelGGL(k_key_dist<uint64_t>, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         keys_s, n, cbits, dist_s);
     } else {
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_dist, dist_s,
                                                  idx_in, idx_out, (int)n, 0, end_bit, s));
@@ -510,9 +538,9 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   // initial active list
   hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                      d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
-                     d_res, d_meta, 1, d_lpx, ctx->work_count);
-  int32_t* h_meta = nullptr;
-  HIP_TRY(hipHostMalloc((void**)&h_meta, 16, hipHostMallocDefault));
+                     d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
+  if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 16, hipHostMallocDefault));
+  int32_t* h_meta = ctx->h_meta;
   int rounds = 0, batch = 2, rc = 0;
   while (true) {
     for (int b = 0; b < batch; ++b) {
@@ -533,8 +561,11 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       }
       {
         ProfScope ps(ctx, "disp_reduce", 0);
+        // single rank: the reduce kernel steps the state machines too; with
+        // a cross-rank all-reduce in between, k_seg_update steps them
         hipLaunchKernelGGL(k_seg_reduce, dim3((S + 3) / 4), dim3(256), 0, s,
-                           d_partial, d_slb, d_sle, S, d_total);
+                           d_partial, d_slb, d_sle, S, d_total,
+                           reduce ? nullptr : d_st, d_flags, d_nrep, C, d_res);
       }
       if (reduce && reduce(d_total, S, user)) {
         rc = fail(H3D_EHIP, "allreduce callback failed");
@@ -544,7 +575,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         ProfScope ps(ctx, "disp_update", 0);
         hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                            d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb,
-                           d_sle, d_res, d_meta, 0, d_lpx, ctx->work_count);
+                           d_sle, d_res, d_meta, 0, reduce ? 1 : 0, d_lpx, ctx->work_count);
       }
       ++rounds;
     }
@@ -563,7 +594,6 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     }
     batch = std::min(batch * 2, 8);
   }
-  (void)hipHostFree(h_meta);
   if (rc) return rc;
   std::vector<int32_t> fl(S);
   HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));

@@ -70,6 +70,28 @@ __global__ void k_gather_soa(const int32_t* __restrict__ perm,
                              const double* __restrict__ f, int64_t n, int R,
                              int32_t* __restrict__ raw_s,
                              double* __restrict__ f_s) {
+  if (R == 4 && ((uintptr_t)raw & 15) == 0 && ((uintptr_t)f & 15) == 0) {
+    // the common shape: one 16 B load of the raw row, two 16 B loads of the
+    // f row per pixel (rows are 16 B aligned), so the random row gather
+    // issues 3 memory instructions per lane instead of 8
+    const int4* raw4 = reinterpret_cast<const int4*>(raw);
+    const double2* f2 = reinterpret_cast<const double2*>(f);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t src = perm[i];
+      const int4 rv = raw4[src];
+      const double2 fa = f2[2 * src], fb = f2[2 * src + 1];
+      raw_s[i] = rv.x;
+      raw_s[n + i] = rv.y;
+      raw_s[2 * n + i] = rv.z;
+      raw_s[3 * n + i] = rv.w;
+      f_s[i] = fa.x;
+      f_s[n + i] = fa.y;
+      f_s[2 * n + i] = fb.x;
+      f_s[3 * n + i] = fb.y;
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t src = perm[i];
@@ -80,26 +102,38 @@ __global__ void k_gather_soa(const int32_t* __restrict__ perm,
   }
 }
 
-// 64-bit sort key (distance, total count): inside a distance segment pixels
-// of similar depth sit in the same wave, so the q2qnbinom branches (tail
-// side, series vs continued fraction) diverge less
+// sort key (distance, total count capped to cbits bits): inside a distance
+// segment pixels of similar depth sit in the same wave, so the q2qnbinom
+// branches (tail side, series vs continued fraction) diverge less. The count
+// only orders pixels inside a segment (which segment a pixel joins is fixed
+// by the distance bits), so capping it changes no result beyond the order of
+// the segment's partial sums. K = uint32_t (16 count bits) whenever the
+// distance fits the other 16: fewer radix passes over half the key bytes.
+template <typename K>
 __global__ void k_dist_count_keys(const int32_t* __restrict__ dist,
                                   const int32_t* __restrict__ raw, int64_t n,
-                                  int R, uint64_t* __restrict__ keys) {
+                                  int R, int cbits, K* __restrict__ keys) {
+  const uint64_t cap = (1ull << cbits) - 1ull;
+  // distances outside the key's range (incl. negative ones) saturate to the
+  // largest code, which is >= D: the caller's segment check rejects them
+  const uint64_t dcap = (uint64_t)(K)~(K)0 >> cbits;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t tot = 0;
     for (int r = 0; r < R; ++r) tot += (uint32_t)raw[i * R + r];
-    if (tot > 0xffffffffull) tot = 0xffffffffull;
-    keys[i] = ((uint64_t)(uint32_t)dist[i] << 32) | tot;
+    if (tot > cap) tot = cap;
+    uint64_t d = (uint32_t)dist[i];
+    if (d > dcap) d = dcap;
+    keys[i] = (K)((d << cbits) | tot);
   }
 }
 
-__global__ void k_key_dist(const uint64_t* __restrict__ keys, int64_t n,
+template <typename K>
+__global__ void k_key_dist(const K* __restrict__ keys, int64_t n, int cbits,
                            int32_t* __restrict__ dist_s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
-    dist_s[i] = (int32_t)(keys[i] >> 32);
+    dist_s[i] = (int32_t)((uint64_t)keys[i] >> cbits);
 }
 
 // seg_start[d] = first index with dist_s >= d (d = 0..D)
@@ -270,10 +304,18 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
 
 // seg_total[s] = sum of the segment's wave partials in list order (one wave
 // per segment, fixed reduction tree -> deterministic)
+// With `st` non-null (no cross-rank reduction between the two steps), the
+// wave then advances its segment's qcml/Brent state machine itself: the
+// segments step in parallel across the chip instead of inside the single
+// list-building workgroup of k_seg_update.
 __global__ void k_seg_reduce(const double* __restrict__ partial,
                              const int32_t* __restrict__ seg_lb,
                              const int32_t* __restrict__ seg_le, int S,
-                             double* __restrict__ seg_total) {
+                             double* __restrict__ seg_total,
+                             SegState* __restrict__ st,
+                             const int* __restrict__ seg_flags,
+                             const int32_t* __restrict__ n_rep, int C,
+                             double* __restrict__ result) {
   const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (s >= S) return;
@@ -283,11 +325,23 @@ __global__ void k_seg_reduce(const double* __restrict__ partial,
   for (int64_t j = b + lane; j < e; j += 64) v += partial[j];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if (lane == 0) seg_total[s] = v;
+  if (lane == 0) {
+    seg_total[s] = v;
+    if (st) {
+      SegState cur = st[s];
+      if (cur.phase != kDone) {
+        cur.flags |= seg_flags[s];
+        seg_step(&cur, v, n_rep[s % C]);
+        st[s] = cur;
+        if (cur.phase == kDone) result[s] = cur.result;
+      }
+    }
+  }
 }
 
-// One workgroup: advance every active segment's qcml/Brent state machine with
-// its (possibly rank-reduced) total, then rebuild the active work list.
+// One workgroup: with `step`, advance every active segment's qcml/Brent
+// state machine with its (rank-reduced) total -- otherwise k_seg_reduce has
+// already stepped them -- then rebuild the active work list.
 __global__ __launch_bounds__(1024) void k_seg_update(
     SegState* __restrict__ st, const double* __restrict__ seg_total,
     const int* __restrict__ seg_flags, int S, int C,
@@ -295,73 +349,124 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     const int32_t* __restrict__ seg_chunk_e, int32_t* __restrict__ list,
     int32_t* __restrict__ seg_lb,
     int32_t* __restrict__ seg_le, double* __restrict__ result,
-    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first,
+    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first, int step,
     const int64_t* __restrict__ seg_px /* this rank's pixels per segment */,
     unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
-  __shared__ int32_t scan[1024];
-  __shared__ int32_t base_s;
-  __shared__ unsigned long long wc[2];
-  if (threadIdx.x == 0) {
-    base_s = 0;
-    wc[0] = wc[1] = 0ull;
-  }
-  __syncthreads();
-  // advance the state machines; count the pixel-replicates the next round's
-  // passes will visit (measurement: algorithmic bytes of the disp kernels)
+  // Every cross-thread step is a wave shuffle tree plus one LDS slot per wave
+  // (16 waves): no contended LDS atomics, two barriers per 1024 segments.
+  constexpr int kW = 1024 / 64;
+  __shared__ unsigned long long wsum[2][kW];
+  __shared__ int32_t wscan[2][kW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // 1. advance the state machines; count the equalize / NLL items of the next
+  // round, and the pixel-replicates they visit (measurement: algorithmic bytes
+  // of the disp kernels)
   unsigned long long weq = 0ull, wnll = 0ull;
+  int ceq = 0;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    SegState cur = st[s];
-    if (!first && cur.phase != kDone) {
-      cur.flags |= seg_flags[s];
-      seg_step(&cur, seg_total[s], n_rep[s % C]);
-      st[s] = cur;
+    int phase;
+    if (!first && step) {
+      SegState cur = st[s];
+      if (cur.phase != kDone) {
+        cur.flags |= seg_flags[s];
+        seg_step(&cur, seg_total[s], n_rep[s % C]);
+        st[s] = cur;
+        if (cur.phase == kDone) result[s] = cur.result;
+      }
+      phase = cur.phase;
+    } else {
+      // stepped by k_seg_reduce (or nothing to step yet)
+      phase = st[s].phase;
+      if (first && phase == kDone) result[s] = st[s].result;
     }
-    if (cur.phase == kDone) result[s] = cur.result;
     const unsigned long long w = (unsigned long long)seg_px[s] * n_rep[s % C];
-    if (cur.phase == kEqualize) weq += w;
-    if (cur.phase == kNll) wnll += w;
-  }
-  if (weq) atomicAdd(&wc[0], weq);
-  if (wnll) atomicAdd(&wc[1], wnll);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    work_count[0] += wc[0];
-    work_count[1] += wc[1];
-  }
-  // list: equalize items of every segment first, then the NLL items
-  for (int pass = 0; pass < 2; ++pass) {
-  const int want = pass == 0 ? kEqualize : kNll;
-  for (int s0 = 0; s0 < S; s0 += blockDim.x) {
-    const int s = s0 + threadIdx.x;
-    int cnt = 0;
-    if (s < S && st[s].phase == want)
-      cnt = seg_chunk_e[s / C] - seg_chunk_b[s / C];
-    scan[threadIdx.x] = cnt;
-    __syncthreads();
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // inclusive scan
-      const int v = (threadIdx.x >= (unsigned)off) ? scan[threadIdx.x - off] : 0;
-      __syncthreads();
-      scan[threadIdx.x] += v;
-      __syncthreads();
+    if (phase == kEqualize) {
+      weq += w;
+      ceq += seg_chunk_e[s / C] - seg_chunk_b[s / C];
     }
-    const int base = base_s;
-    const int beg = base + scan[threadIdx.x] - cnt;
-    if (s < S && (cnt > 0 || pass == 0)) {
+    if (phase == kNll) wnll += w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    weq += __shfl_xor(weq, off, 64);
+    wnll += __shfl_xor(wnll, off, 64);
+    ceq += __shfl_xor(ceq, off, 64);
+  }
+  if (lane == 0) {
+    wsum[0][wid] = weq;
+    wsum[1][wid] = wnll;
+    wscan[0][wid] = ceq;
+  }
+  __syncthreads();
+  int eq_total = 0;
+#pragma unroll
+  for (int w = 0; w < kW; ++w) eq_total += wscan[0][w];
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0ull, b = 0ull;
+    for (int w = 0; w < kW; ++w) {
+      a += wsum[0][w];
+      b += wsum[1][w];
+    }
+    work_count[0] += a;
+    work_count[1] += b;
+  }
+  // 2. list: the equalize items of every segment first (offsets from 0), then
+  // the NLL items (offsets from eq_total); one pass, both counts scanned at
+  // once per 1024-segment slab
+  int base_eq = 0, base_nll = eq_total;
+  for (int s0 = 0; s0 < S; s0 += blockDim.x) {
+    __syncthreads();  // wscan reuse
+    const int s = s0 + threadIdx.x;
+    int phase = kDone, cnt = 0;
+    if (s < S) {
+      phase = st[s].phase;
+      cnt = seg_chunk_e[s / C] - seg_chunk_b[s / C];
+    }
+    const int ce = (phase == kEqualize) ? cnt : 0;
+    const int cn = (phase == kNll) ? cnt : 0;
+    int ie = ce, in = cn;  // inclusive wave scans
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int ue = __shfl_up(ie, off, 64), un = __shfl_up(in, off, 64);
+      if (lane >= off) {
+        ie += ue;
+        in += un;
+      }
+    }
+    if (lane == 63) {
+      wscan[0][wid] = ie;
+      wscan[1][wid] = in;
+    }
+    __syncthreads();
+    int pe = 0, pn = 0, te = 0, tn = 0;
+#pragma unroll
+    for (int w = 0; w < kW; ++w) {
+      const int ve = wscan[0][w], vn = wscan[1][w];
+      if (w < wid) {
+        pe += ve;
+        pn += vn;
+      }
+      te += ve;
+      tn += vn;
+    }
+    if (s < S) {
+      const bool eq = phase == kEqualize;
+      const int beg = eq ? base_eq + pe + ie - ce : base_nll + pn + in - cn;
+      const int c_here = eq ? ce : cn;
+      // finished segments keep an empty range (k_seg_reduce writes 0)
       seg_lb[s] = beg;
-      seg_le[s] = beg + cnt;
+      seg_le[s] = beg + c_here;
       const int d = s / C, c = s % C;
       const int cb = seg_chunk_b[d];
-      for (int j = 0; j < cnt; ++j) list[beg + j] = (cb + j) * C + c;
+      for (int j = 0; j < c_here; ++j) list[beg + j] = (cb + j) * C + c;
     }
-    __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) base_s = base + scan[threadIdx.x];
-    __syncthreads();
-  }
-  if (pass == 0 && threadIdx.x == 0) meta[2] = base_s;
+    base_eq += te;
+    base_nll += tn;
   }
   if (threadIdx.x == 0) {
-    meta[0] = base_s;
-    meta[1] = base_s;
+    meta[0] = base_nll;
+    meta[1] = base_nll;
+    meta[2] = eq_total;
   }
 }
 
