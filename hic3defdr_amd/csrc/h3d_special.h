@@ -31,8 +31,12 @@
 
 #if defined(__HIPCC__)
 #define H3D_HD __host__ __device__ inline
+// a rarely taken path kept out of line, so its temporaries do not raise the
+// register demand of the kernels that inline everything else
+#define H3D_HD_COLD __host__ __device__ __attribute__((noinline))
 #else
 #define H3D_HD inline
+#define H3D_HD_COLD inline
 #endif
 
 // Work counters for tools/q2q_stats (host builds with H3D_INSTRUMENT only;
@@ -306,8 +310,10 @@ H3D_HD double igam_series(double a, double x) {
   return igam_series_sum(a, x) * ax / a;
 }
 
-// Q(a, x) for small x without cancellation (DLMF 8.7.3), given lga.
-H3D_HD double igamc_series_l(double a, double x, double lga) {
+// Q(a, x) for small x without cancellation (DLMF 8.7.3), given lga. Out of
+// line: taken by < 1% of the equalize lanes, but inlined its lgam1p Taylor
+// table doubled the equalize kernel's spills (224 -> 112 B/lane at W=4).
+H3D_HD_COLD double igamc_series_l(double a, double x, double lga) {
   double fac = 1.0, sum = 0.0;
   for (int n = 1; n < kMaxIter; ++n) {
     H3D_STAT(su_it, 1);
@@ -663,35 +669,30 @@ H3D_HD bool igam_taylor_ok(double a, double xe, double h) {
          fabs(a - 1.0) * u * u <= 0.25;
 }
 
+// The coefficients follow from the ODE y' = g'(s) y, g'(s) = b / (xe + s) - 1
+// (b = a - 1): (xe + s) y' = (b - xe - s) y gives the three-term recurrence
+//   e_(k+1) = ((b - xe - k) e_k - e_(k-1)) / (xe (k + 1)),  e_(-1) = 0,
+// i.e. in the scaled E_k = e_k h^k (s = h t, t in [0, 1])
+//   E_(k+1) = u ((b - xe - k) E_k - h E_(k-1)) / (k + 1),  u = h / xe.
+// Both terms decay (ratios ~ -u and ~ -h / k), so the forward recursion is
+// stable; only two coefficients are live at a time (the convolution form of
+// the power-series exponential kept all 2K + 1 in registers).
 H3D_HD void igam_step_taylor(double a, double xe, double h, double* dint,
                              double* ratio) {
   constexpr int K = kTaylorK;
-  constexpr double inv[K + 2] = {0.0, 1.0, 1.0 / 2, 1.0 / 3, 1.0 / 4,
-                                 1.0 / 5, 1.0 / 6, 1.0 / 7, 1.0 / 8, 1.0 / 9,
-                                 1.0 / 10, 1.0 / 11, 1.0 / 12, 1.0 / 13};
   const double b = a - 1.0;
-  // work in s = h t (t in [0, 1]): c_j = g_j h^j, so every coefficient is
-  // O(rho^j) and exp(g(h t)) = sum E_k t^k with E_k = e_k h^k
   const double u = h / xe;
-  double jc[K + 1];  // j * c_j
-  double pw = u;
-  for (int j = 1; j <= K; ++j) {
-    jc[j] = (j & 1) ? b * pw : -b * pw;
-    pw *= u;
-  }
-  jc[1] -= h;
-  double E[K + 1];
-  E[0] = 1.0;
-  for (int k = 1; k <= K; ++k) {
-    double acc = 0.0;
-    for (int j = 1; j <= k; ++j) acc += jc[j] * E[k - j];
-    E[k] = acc * inv[k];
-  }
+  const double c0 = b - xe;
+  double em1 = 0.0, e = 1.0;
   // integral_0^h = h sum E_k / (k+1); exp(g(h)) = sum E_k
-  double in = 0.0, ex = 0.0;
-  for (int k = K; k >= 0; --k) {
-    in += E[k] * inv[k + 1];
-    ex += E[k];
+  double in = 1.0, ex = 1.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double en = u * ((c0 - k) * e - h * em1) * (1.0 / (k + 1));
+    em1 = e;
+    e = en;
+    in += e * (1.0 / (k + 2));
+    ex += e;
   }
   *dint = in * h;
   *ratio = ex;
