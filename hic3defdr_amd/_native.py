@@ -24,7 +24,8 @@ EXPORTS = [
     'h3d_size_factors_cmor', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
     'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
-    'h3d_find_clusters', 'h3d_format_clusters',
+    'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
+    'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel',
 ]
 
 
@@ -81,6 +82,12 @@ def load_library(path=None):
             'h3d_find_clusters': (_I, [_P, _P, _I64, _I, _P, _P]),
             'h3d_format_clusters': (_I, [_P, _P, _P, _P, _I64, _P, _I64, _P,
                                          _P]),
+            'h3d_lrt_poisson': (_I, [_P, _P, _P, _I64, _I, _I, _P, _P, _P,
+                                     _P, _P]),
+            'h3d_lrt_poisson_dev': (_I, [_P, _P, _P, _I64, _I, _I, _P, _P,
+                                         _P, _P, _P]),
+            'h3d_mme_per_pixel': (_I, [_P, _P, _P, _I64, _I, _I, _P, _D,
+                                       _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -250,6 +257,43 @@ class Context(object):
             self.handle, d_raw, d_f, d_dist, _ptr(tab), n, R, C, _ptr(cond),
             D, int(bool(refit_mu)), d_p, d_llr, d_mu0, d_mu1, d_disp),
             'h3d_lrt_dev')
+
+    # -- alternative models (analysis/alternatives.py) -----------------------
+    def lrt_poisson(self, raw, f, cond_of_rep, C):
+        """Poisson LRT (alternatives.py:25-42, refit_mu=True): p, llr,
+        mu_hat_null (n,), mu_hat_alt (n, C)."""
+        raw = _c(raw, np.int64)
+        f = _c(f, np.float64)
+        cond = _c(cond_of_rep, np.int32)
+        n, R = raw.shape
+        p = np.empty(n)
+        llr = np.empty(n)
+        mu0 = np.empty(n)
+        mu1 = np.empty((n, C))
+        _check(self.lib.h3d_lrt_poisson(
+            self.handle, _ptr(raw), _ptr(f), n, R, C, _ptr(cond), _ptr(p),
+            _ptr(llr), _ptr(mu0), _ptr(mu1)), 'h3d_lrt_poisson')
+        return p, llr, mu0, mu1
+
+    def lrt_poisson_dev(self, d_raw, d_f, n, R, cond_of_rep, C, d_p, d_llr,
+                        d_mu0, d_mu1):
+        cond = _c(cond_of_rep, np.int32)
+        _check(self.lib.h3d_lrt_poisson_dev(
+            self.handle, d_raw, d_f, n, R, C, _ptr(cond), d_p, d_llr, d_mu0,
+            d_mu1), 'h3d_lrt_poisson_dev')
+
+    def mme_per_pixel(self, data, f, cond_of_rep, C, min_disp=-np.inf):
+        """Per-pixel MME dispersion of each condition (dispersion.py:83-104)
+        floored at ``min_disp`` (NaN stays NaN): (n, C)."""
+        data = _c(data, np.float64)
+        f = _c(f, np.float64) if f is not None else None
+        cond = _c(cond_of_rep, np.int32)
+        n, R = data.shape
+        out = np.empty((n, C))
+        _check(self.lib.h3d_mme_per_pixel(
+            self.handle, _ptr(data), _ptr(f), n, R, C, _ptr(cond),
+            float(min_disp), _ptr(out)), 'h3d_mme_per_pixel')
+        return out
 
     # -- measurement ---------------------------------------------------------
     def profile(self, on=True, level=2):

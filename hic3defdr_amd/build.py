@@ -20,9 +20,11 @@ HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 
 # (source, compiler): device TU through hipcc, host-only TUs through g++
-NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_calls.cpp', 'g++')]
+NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
+               ('h3d_calls.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
-           'h3d_prepare.h', 'h3d_prepare_api.h', 'h3d_errors.h']
+           'h3d_prepare.h', 'h3d_prepare_api.h', 'h3d_errors.h',
+           'h3d_ctx.h']
 
 
 def _stale(target, deps):

@@ -12,65 +12,17 @@
 #include <vector>
 
 #include "h3d.h"
+#include "h3d_ctx.h"
 #include "h3d_errors.h"
 #include "h3d_host.h"
 #include "h3d_kernels.h"
 #include "h3d_prepare.h"
 
 using namespace h3d;
-
-namespace {
-
+using namespace h3dint;
 using h3derr::fail;
 
-#define HIP_TRY(expr)                                                      \
-  do {                                                                     \
-    hipError_t e_ = (expr);                                                \
-    if (e_ != hipSuccess)                                                  \
-      return fail(H3D_EHIP, "%s failed: %s (%s:%d)", #expr,                \
-                  hipGetErrorString(e_), __FILE__, __LINE__);              \
-  } while (0)
-
-struct ProfEntry {
-  double ms = 0.0;
-  int64_t launches = 0;
-  int64_t units = 0;
-};
-
-}  // namespace
-
-struct h3d_ctx {
-  int device = 0;
-  hipStream_t own = nullptr;
-  hipStream_t stream = nullptr;
-  int n_cu = 256;
-  std::map<const void*, int> resident;  // kernel -> resident workgroups / CU
-  // 0 off; 1: the roofline kernels only ("disp_work", "lrt"); 2: every
-  // scope. Events are collected lazily (profile_read / reset / close), so
-  // the launch path never waits on them.
-  int prof = 0;
-  std::map<std::string, ProfEntry> stats;
-  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
-  std::vector<int64_t> pending_units;
-  std::vector<hipEvent_t> event_pool;
-  // grow-only device scratch, by slot
-  std::map<std::string, std::pair<void*, size_t>> bufs;
-  // prepare_data state between h3d_union_count and h3d_union_fill
-  PrepUnion prep;
-  // [equalize, nll] pixel-replicates processed by disp_work (measurement)
-  unsigned long long* work_count = nullptr;
-  // pinned host word the disp loop polls (active work items), kept for the
-  // ctx's lifetime (a per-call hipHostFree would synchronise the device)
-  int32_t* h_meta = nullptr;
-  // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
-  // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
-  // 1 (distance, total count)
-  int disp_w = 4;  // measured best (sweep at 7413b12, equalize ms/step for
-                   // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
-  int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
-};
-
-namespace {
+namespace h3dint {
 
 void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes) {
   auto& b = ctx->bufs[slot];
@@ -96,36 +48,6 @@ hipEvent_t ev_get(h3d_ctx* ctx) {
   return e;
 }
 
-void prof_collect(h3d_ctx* ctx);
-
-// wraps one kernel launch with HIP events on the ctx stream when profiling
-struct ProfScope {
-  h3d_ctx* ctx;
-  const char* name;
-  int64_t units;
-  hipEvent_t a = nullptr, b = nullptr;
-  bool on;
-  ProfScope(h3d_ctx* c, const char* n, int64_t u, int level = 2)
-      : ctx(c), name(n), units(u), on(c->prof >= level) {
-    // bound the pending list (collecting synchronises the stream)
-    if (on && ctx->pending.size() > 16384) prof_collect(ctx);
-    if (on) {
-      a = ev_get(ctx);
-      b = ev_get(ctx);
-      (void)hipEventRecord(a, ctx->stream);
-    }
-  }
-  ~ProfScope() {
-    if (on) {
-      (void)hipEventRecord(b, ctx->stream);
-      ctx->pending.push_back({name, {a, b}});
-      ctx->pending_units.push_back(units);
-    }
-  }
-};
-
-
-
 void prof_collect(h3d_ctx* ctx) {
   if (ctx->pending.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
@@ -144,7 +66,7 @@ void prof_collect(h3d_ctx* ctx) {
   ctx->pending_units.clear();
 }
 
-int grid_for(h3d_ctx* ctx, int64_t n, int per_cu = 8) {
+int grid_for(h3d_ctx* ctx, int64_t n, int per_cu) {
   int64_t g = (n + kBlock - 1) / kBlock;
   g = std::min<int64_t>(g, (int64_t)ctx->n_cu * per_cu);
   return (int)std::max<int64_t>(g, 1);
@@ -166,6 +88,10 @@ int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
     if ((*nrep)[c] == 0) return fail(H3D_EARG, "condition %d has no replicates", c);
   return 0;
 }
+
+}  // namespace h3dint
+
+namespace {
 
 // workgroups of `kernel` that fit on one CU at once (queried once per kernel;
 // every device of a process is a gfx950)

@@ -1,0 +1,127 @@
+// libh3d internals shared by its HIP translation units (h3d_api.hip: the hot
+// path; h3d_alt.hip: the alternative models): the context behind the C ABI's
+// opaque h3d_ctx handle and the launch helpers. Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "h3d.h"
+#include "h3d_errors.h"
+
+#define HIP_TRY(expr)                                                      \
+  do {                                                                     \
+    hipError_t e_ = (expr);                                                \
+    if (e_ != hipSuccess)                                                  \
+      return h3derr::fail(H3D_EHIP, "%s failed: %s (%s:%d)", #expr,        \
+                          hipGetErrorString(e_), __FILE__, __LINE__);      \
+  } while (0)
+
+namespace h3d {
+
+// prepare_data state between h3d_union_count and h3d_union_fill
+struct PrepUnion {
+  int R = 0, n_bins = 0;
+  int64_t n_entries = 0, n_px = 0;
+  // device
+  int64_t* keys_sorted = nullptr;  // n_entries
+  int32_t* ent_sorted = nullptr;   // n_entries
+  int32_t* run_of = nullptr;       // n_entries (exclusive-scanned heads)
+  int32_t* px_of_run = nullptr;    // runs -> pixel (or -1)
+  int64_t* run_start = nullptr;    // runs + 1
+  double* ent_val = nullptr;       // raw value per entry (summed duplicates not needed: canonical CSR)
+  int32_t* ent_rep = nullptr;      // replicate per entry
+  double* bias = nullptr;          // (n_bins, R)
+  int64_t n_runs = 0;
+};
+
+}  // namespace h3d
+
+namespace h3dint {
+
+struct ProfEntry {
+  double ms = 0.0;
+  int64_t launches = 0;
+  int64_t units = 0;
+};
+
+}  // namespace h3dint
+
+struct h3d_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int n_cu = 256;
+  std::map<const void*, int> resident;  // kernel -> resident workgroups / CU
+  // 0 off; 1: the roofline kernels only ("disp_work", "lrt"); 2: every
+  // scope. Events are collected lazily (profile_read / reset / close), so
+  // the launch path never waits on them.
+  int prof = 0;
+  std::map<std::string, h3dint::ProfEntry> stats;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<int64_t> pending_units;
+  std::vector<hipEvent_t> event_pool;
+  // grow-only device scratch, by slot
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  // prepare_data state between h3d_union_count and h3d_union_fill
+  h3d::PrepUnion prep;
+  // [equalize, nll] pixel-replicates processed by disp_work (measurement)
+  unsigned long long* work_count = nullptr;
+  // pinned host word the disp loop polls (active work items), kept for the
+  // ctx's lifetime (a per-call hipHostFree would synchronise the device)
+  int32_t* h_meta = nullptr;
+  // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
+  // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
+  // 1 (distance, total count)
+  int disp_w = 4;  // measured best (sweep at 7413b12, equalize ms/step for
+                   // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
+  int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
+};
+
+namespace h3dint {
+
+constexpr int kLaunchBlock = 256;
+
+// grow-only device buffer of the ctx, by slot name (nullptr on OOM)
+void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes);
+hipEvent_t ev_get(h3d_ctx* ctx);
+// folds the recorded event pairs into ctx->stats (synchronises the stream)
+void prof_collect(h3d_ctx* ctx);
+// grid of a grid-stride elementwise kernel over n items
+int grid_for(h3d_ctx* ctx, int64_t n, int per_cu = 8);
+// validates a replicate -> condition map; per-condition replicate counts and
+// replicate indices (C x kMaxReps, design order)
+int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
+               std::vector<int32_t>* rep_idx);
+
+// wraps one kernel launch with HIP events on the ctx stream when profiling
+struct ProfScope {
+  h3d_ctx* ctx;
+  const char* name;
+  int64_t units;
+  hipEvent_t a = nullptr, b = nullptr;
+  bool on;
+  ProfScope(h3d_ctx* c, const char* n, int64_t u, int level = 2)
+      : ctx(c), name(n), units(u), on(c->prof >= level) {
+    // bound the pending list (collecting synchronises the stream)
+    if (on && ctx->pending.size() > 16384) prof_collect(ctx);
+    if (on) {
+      a = ev_get(ctx);
+      b = ev_get(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~ProfScope() {
+    if (on) {
+      (void)hipEventRecord(b, ctx->stream);
+      ctx->pending.push_back({name, {a, b}});
+      ctx->pending_units.push_back(units);
+    }
+  }
+};
+
+}  // namespace h3dint

@@ -18,20 +18,7 @@
 
 namespace h3d {
 
-struct PrepUnion {
-  int R = 0, n_bins = 0;
-  int64_t n_entries = 0, n_px = 0;
-  // device
-  int64_t* keys_sorted = nullptr;  // n_entries
-  int32_t* ent_sorted = nullptr;   // n_entries
-  int32_t* run_of = nullptr;       // n_entries (exclusive-scanned heads)
-  int32_t* px_of_run = nullptr;    // runs -> pixel (or -1)
-  int64_t* run_start = nullptr;    // runs + 1
-  double* ent_val = nullptr;       // raw value per entry (summed duplicates not needed: canonical CSR)
-  int32_t* ent_rep = nullptr;      // replicate per entry
-  double* bias = nullptr;          // (n_bins, R)
-  int64_t n_runs = 0;
-};
+// (the union state PrepUnion lives in h3d_ctx.h, inside the h3d_ctx)
 
 // row id of every CSR entry (one thread per row)
 __global__ void k_csr_rows(const int64_t* __restrict__ indptr, int n_bins,

@@ -33,7 +33,7 @@
 #define H3D_HD __host__ __device__ inline
 // a rarely taken path kept out of line, so its temporaries do not raise the
 // register demand of the kernels that inline everything else
-#define H3D_HD_COLD __host__ __device__ __attribute__((noinline))
+#define H3D_HD_COLD __host__ __device__ inline __attribute__((noinline))
 #else
 #define H3D_HD inline
 #define H3D_HD_COLD inline

@@ -20,6 +20,11 @@
  *                              classify, analysis.py:366-486)
  *   h3d_format_clusters    <- util/clusters.py:129-130 save_clusters text,
  *                              util/cluster_table.py:67 "cluster" column
+ *   h3d_lrt_poisson        <- analysis/alternatives.py:17-42 poisson_lrt
+ *                              (Poisson3DeFDR.lrt, :73-115)
+ *   h3d_mme_per_pixel      <- util/dispersion.py:83-104 mme_per_pixel
+ *                              (Unsmoothed3DeFDR.estimate_disp,
+ *                              alternatives.py:119-137)
  *
  * Conventions: 0 on success, a negative H3D_E* code otherwise (the message is
  * in h3d_last_error(), thread-local). Host buffers are C-contiguous and owned
@@ -161,6 +166,32 @@ int h3d_format_clusters(const int64_t* row, const int64_t* col,
                         const int64_t* order, const int64_t* starts,
                         int64_t n_clusters, char* buf, int64_t cap,
                         int64_t* ends, int64_t* len);
+
+/* ---- alternative models (analysis/alternatives.py) ---------------------- */
+
+/* Poisson LRT (alternatives.py:25-42 with refit_mu=True, the only mode
+ * Poisson3DeFDR uses and the only one the reference can run: its refit_mu=False
+ * branch builds mu_hat_alt transposed and fails in np.dot). mu0 =
+ * np.average(raw / f, weights=f) over all replicates, mu1[:, c] the same over
+ * condition c's; llr = sum log poisson.pmf(raw | mu0 f) - sum log
+ * poisson.pmf(raw | mu1[cond] f); p = chi2(C - 1).sf(-2 llr). raw/f (n, R) ->
+ * p, llr, mu0 (n), mu1 (n, C). */
+int h3d_lrt_poisson(h3d_ctx* ctx, const int64_t* raw, const double* f,
+                    int64_t n, int R, int C, const int32_t* cond_of_rep,
+                    double* p, double* llr, double* mu0, double* mu1);
+int h3d_lrt_poisson_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                        int64_t n, int R, int C, const int32_t* cond_of_rep,
+                        double* d_p, double* d_llr, double* d_mu0,
+                        double* d_mu1);
+
+/* Per-pixel method-of-moments dispersion of every condition's replicates
+ * (dispersion.py:83-104 mme_per_pixel(data[:, design[:, c]], f)): data (n, R)
+ * (divided by f (n, R) when f != NULL) -> disp (n, C) = max((var - mean) /
+ * mean^2, min_disp), var with ddof 1; NaN stays NaN (numpy maximum).
+ * min_disp = -inf for no floor; Unsmoothed3DeFDR uses 1e-7. */
+int h3d_mme_per_pixel(h3d_ctx* ctx, const double* data, const double* f,
+                      int64_t n, int R, int C, const int32_t* cond_of_rep,
+                      double min_disp, double* disp);
 
 /* ---- measurement -------------------------------------------------------- */
 
