@@ -632,6 +632,23 @@ def lrt(raw, f, disp, design, refit_mu=True, faithful=False):
     return pvalues, llr, mu_hat_null, mu_hat_alt
 
 
+def poisson_lrt(raw, f, design):
+    """``alternatives.py:17-42`` with refit_mu=True (the reference's False
+    branch builds mu_hat_alt transposed and fails in np.dot)."""
+    from scipy import stats
+    design = np.asarray(design, dtype=bool)
+    mu0 = np.average(raw / f, weights=f, axis=1)
+    mu1 = np.array([np.average(raw[:, design[:, c]] / f[:, design[:, c]],
+                               weights=f[:, design[:, c]], axis=1)
+                    for c in range(design.shape[1])]).T
+    wide = np.dot(mu1, design.T)
+    null_ll = np.sum(stats.poisson(mu0[:, None] * f).logpmf(raw), axis=1)
+    alt_ll = np.sum(stats.poisson(wide * f).logpmf(raw), axis=1)
+    llr = null_ll - alt_ll
+    p = stats.chi2(design.shape[1] - 1).sf(-2 * llr)
+    return p, llr, mu0, mu1
+
+
 # --------------------------------------------------------------------------
 # pipeline driver — reference analysis/analysis.py + analysis/core.py
 # --------------------------------------------------------------------------

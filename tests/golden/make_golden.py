@@ -346,9 +346,54 @@ def unit_clusters():
     np.savez_compressed(os.path.join(HERE, 'unit_clusters.npz'), **out)
 
 
+ALT_STAGES = ['disp', 'pvalues', 'llr', 'mu_hat_null', 'mu_hat_alt',
+              'qvalues', 'loop_idx']
+
+
+def run_alternatives(name='small2'):
+    """Poisson3DeFDR / Unsmoothed3DeFDR / Global3DeFDR (alternatives.py)
+    run_to_qvalues on the committed e2e inputs: every outdir array they
+    write, in alt_<name>.npz as <class>__<stage>__<chrom>."""
+    from hic3defdr.analysis import alternatives
+    sizes, dmax, npc, seed, loops = E2E[name]
+    base = os.path.join(HERE, 'data', name)
+    g = np.load(os.path.join(HERE, 'e2e_%s.npz' % name))
+    reps = [str(r) for r in g['meta_reps']]
+    conds = [str(c) for c in g['meta_conds']]
+    chroms = [str(c) for c in g['meta_chroms']]
+    design = pd.DataFrame(g['meta_design'].astype(bool), index=reps,
+                          columns=conds)
+    lp = {c: os.path.join(base, 'clusters', '%s_<chrom>.json' % c)
+          for c in conds} if loops else None
+    out = {}
+    for cls in ('Poisson3DeFDR', 'Unsmoothed3DeFDR', 'Global3DeFDR'):
+        outdir = os.path.join('/tmp', 'h3golden_alt_%s_%s' % (cls, name))
+        shutil.rmtree(outdir, ignore_errors=True)
+        h = getattr(alternatives, cls)(
+            raw_npz_patterns=[os.path.join(base, r, '<chrom>_raw.npz')
+                              for r in reps],
+            bias_patterns=[os.path.join(base, r, '<chrom>_kr.bias')
+                           for r in reps],
+            chroms=chroms, design=design, outdir=outdir,
+            dist_thresh_max=dmax, loop_patterns=lp)
+        h.run_to_qvalues(n_threads=0, verbose=False)
+        for chrom in chroms:
+            for st in ALT_STAGES:
+                fn = os.path.join(outdir, '%s_%s.npy' % (st, chrom))
+                if os.path.exists(fn):
+                    out['%s__%s__%s' % (cls, st, chrom)] = np.load(fn)
+        fn = os.path.join(outdir, 'disp_per_dist.npy')
+        if os.path.exists(fn):
+            out['%s__disp_per_dist' % cls] = np.load(fn)
+    np.savez_compressed(os.path.join(HERE, 'alt_%s.npz' % name), **out)
+    print('alternatives', name, sorted(out))
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling',
-                             'calls', 'clusters']
+                             'calls', 'clusters', 'alt']
+    if 'alt' in which:
+        run_alternatives('small2')
     if 'calls' in which:
         for name in E2E:
             run_calls(name)
