@@ -147,6 +147,9 @@ H3D_HD double lgam(double x) {
 // Error ~2 ulp of ln m plus the rounding of e ln 2 -- a few 1e-16 relative,
 // at about half the instructions of the libm-accurate log.
 H3D_HD double log_fast(double x) {
+#if defined(__clang__)
+#pragma clang fp contract(fast)  // used by the NLL lgamma only (see there)
+#endif
   int e;
   double m = frexp(x, &e);  // [0.5, 1)
   if (m < kSqrt1_2) {
@@ -180,13 +183,26 @@ H3D_HD double log_fast(double x) {
 // ln P), relative ~1e-15 above. cephes lgam (scipy gammaln) instead runs a
 // data-dependent recurrence with a division per step below 13, which
 // serialises across a wave.
+//
+// The shift below 10 is a fixed 5 or 10 steps (no data-dependent loop, which
+// serialised the lanes of a wave): P is built from the degree-5 rising
+// factorial x (x+1) (x+2) (x+3) (x+4) = ((((x + 10) x + 35) x + 50) x + 24) x
+// (positive coefficients: no cancellation for x > 0), y lands in [10, 15).
+// FMA contraction is on here: only the absolute error matters (see above).
 H3D_HD double lgam_nll(double x) {
+#if defined(__clang__)
+#pragma clang fp contract(fast)
+#endif
   if (!(x > 0.0)) return (x == 0.0) ? INFINITY : NAN;  // as cephes
   if (is_inf(x)) return x;
   double y = x, P = 1.0;
-  while (y < 10.0) {
-    P *= y;
-    y += 1.0;
+  if (x < 10.0) {
+    const bool two = x < 5.0;
+    const double u = two ? x + 5.0 : x;
+    const double pu = ((((u + 10.0) * u + 35.0) * u + 50.0) * u + 24.0) * u;
+    const double px = ((((x + 10.0) * x + 35.0) * x + 50.0) * x + 24.0) * x;
+    P = two ? px * pu : pu;
+    y = u + 5.0;
   }
   const double r = 1.0 / y, r2 = r * r;
   const double corr =
@@ -199,7 +215,7 @@ H3D_HD double lgam_nll(double x) {
                                          r2 * (1.0 / 156.0 +
                                                r2 * (-3617.0 / 122400.0))))))));
   double v = (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
-  if (P != 1.0) v -= log_fast(P);
+  if (x < 10.0) v -= log_fast(P);
   return v;
 }
 
@@ -339,32 +355,50 @@ H3D_HD double igamc_series(double a, double x) {
 // cross product is exact to ~1 eps of |p_k q_{k-1}|, so the test is met once
 // the convergents agree to ~3 eps (cephes: once they round to the same double).
 H3D_HD double igamc_cf_ratio(double a, double x) {
+#if defined(__clang__)
+  // contraction (the convergents' products fuse into FMAs) -- the ratio
+  // agrees with the uncontracted recurrence to ~1 ulp
+#pragma clang fp contract(fast)
+#endif
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
-  double pkm2 = 1.0, qkm2 = x, pkm1 = x + 1.0, qkm1 = z * x;
-  for (int i = 0; i < kMaxIter; ++i) {
+  // (p1, q1): the latest convergent, (p0, q0): the one before. Two steps per
+  // trip with the roles swapped, so no register moves between steps.
+  double p0 = 1.0, q0 = x, p1 = x + 1.0, q1 = z * x;
+  for (int i = 0; i < kMaxIter / 2; ++i) {
     H3D_STAT(cf_it, 1);
     c += 1.0;
     y += 1.0;
     z += 2.0;
-    const double yc = y * c;
-    const double pk = pkm1 * z - pkm2 * yc;
-    const double qk = qkm1 * z - qkm2 * yc;
-    const double lead = pk * qkm1;
-    const double cross = lead - pkm1 * qk;
-    const bool done = (qk != 0.0) && fabs(cross) <= 4.0 * kMachEp * fabs(lead);
-    pkm2 = pkm1;
-    pkm1 = pk;
-    qkm2 = qkm1;
-    qkm1 = qk;
-    if (fabs(pk) > kBig) {
-      pkm2 *= kBigInv;
-      pkm1 *= kBigInv;
-      qkm2 *= kBigInv;
-      qkm1 *= kBigInv;
+    double yc = y * c;
+    p0 = p1 * z - p0 * yc;  // step A: new latest in (p0, q0)
+    q0 = q1 * z - q0 * yc;
+    double lead = p0 * q1;
+    bool done = (q0 != 0.0) && fabs(lead - p1 * q0) <= 4.0 * kMachEp * fabs(lead);
+    if (fabs(p0) > kBig) {
+      p0 *= kBigInv;
+      q0 *= kBigInv;
+      p1 *= kBigInv;
+      q1 *= kBigInv;
     }
-    if (done) break;
+    if (done) return p0 / q0;
+    H3D_STAT(cf_it, 1);
+    c += 1.0;
+    y += 1.0;
+    z += 2.0;
+    yc = y * c;
+    p1 = p0 * z - p1 * yc;  // step B: new latest in (p1, q1)
+    q1 = q0 * z - q1 * yc;
+    lead = p1 * q0;
+    done = (q1 != 0.0) && fabs(lead - p0 * q1) <= 4.0 * kMachEp * fabs(lead);
+    if (fabs(p1) > kBig) {
+      p0 *= kBigInv;
+      q0 *= kBigInv;
+      p1 *= kBigInv;
+      q1 *= kBigInv;
+    }
+    if (done) return p1 / q1;
   }
-  return pkm1 / qkm1;
+  return p1 / q1;
 }
 
 // Q(a, x) by the continued fraction.
@@ -775,9 +809,14 @@ H3D_HD double igamci(double a, double q) {
 }
 
 // chi2(df).sf(x) as scipy.stats: support lower bound -> 1 (cephes chdtrc).
+// df = 1 and 2 (the LRT with 2 and 3 conditions) use the closed forms
+// Q(1/2, y) = erfc(sqrt(y)) and Q(1, y) = exp(-y) instead of the series /
+// continued fraction (same values to a few ulp).
 H3D_HD double chi2_sf(double df, double x) {
   if (x != x) return NAN;
   if (x <= 0.0) return 1.0;
+  if (df == 1.0) return erfc(sqrt(x / 2.0));
+  if (df == 2.0) return exp(-x / 2.0);
   return igamc(df / 2.0, x / 2.0);
 }
 
