@@ -31,6 +31,32 @@ METRIC = ("pixels/sec through estimate_disp+lrt, 4 reps @10kb; "
           "max-|Δq| vs reference")
 
 
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                           'profiles', 'pmc_traffic_default.json')
+
+
+def pmc_traffic(kernel, bins, dmax):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (tools/pmc_passes.sh over this same default command: FETCH_SIZE x2
+    gfx950 correction + WRITE_SIZE, each its own rocprofv3 pass).  Counters
+    cannot be read inside the timed run, so the figure comes from that
+    profile; None unless the workload is the one it was measured on."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    if d.get('bins') != bins or d.get('dmax') != dmax:
+        return None
+    rd = wr = 0.0
+    n = 0
+    for key, e in d['kernels'].items():
+        if kernel in key.split('[')[0]:
+            rd += e.get('hbm_read_bytes_corrected', 0.0)
+            wr += e.get('hbm_write_bytes', 0.0)
+            n += e['dispatches']
+    return (rd + wr) / n if n else None
+
+
 def bytes_per_lrt_pixel(R, C):
     # raw int32 4R + f 8R + dist 4 in; p, llr, mu0 24 + mu1 8C + disp 8C out
     return 12 * R + 16 * C + 28
@@ -221,7 +247,12 @@ def main():
                 'roofline': {
                     'bound': 'hbm', 'kernel': 'k_disp_work',
                     'achieved': w_ach, 'peak': peak, 'unit': 'GB/s',
-                    'frac': w_ach / peak, 'traffic': None,
+                    'frac': w_ach / peak,
+                    # equalize instantiation <M=4, W=4, kEqualize>
+                    'traffic': pmc_traffic('k_disp_work<4, 4, 0>', args.bins,
+                                           args.dmax),
+                    'traffic_source': 'profiles/pmc_traffic_default.json '
+                                      '(HBM bytes per launch)',
                     'bytes_per_launch': w_bytes / max(w_n, 1),
                     'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
                     'note': 'FP64-VALU/transcendental bound (SURVEY.md '
