@@ -155,6 +155,10 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
   {
     ProfScope ps(ctx, "disp_nll", 0);
     auto k = k_disp_work<M, 1, kNll>;
+    if constexpr (M == 4) {
+      if (ctx->nll_w == 2) k = k_disp_work<M, 2, kNll>;
+      else if (ctx->nll_w == 4) k = k_disp_work<M, 4, kNll>;
+    }
     hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
                        st, seg_flags, list, meta, partial);
@@ -239,6 +243,7 @@ h3d_ctx* h3d_open(int device) {
   ctx->stream = ctx->own;
   if (const char* e = std::getenv("H3D_DISP_W")) ctx->disp_w = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_SORT")) ctx->disp_sort = std::atoi(e);
+  if (const char* e = std::getenv("H3D_NLL_W")) ctx->nll_w = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);

@@ -80,6 +80,7 @@ struct h3d_ctx {
   int disp_w = 4;  // measured best (sweep at 7413b12, equalize ms/step for
                    // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
   int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
+  int nll_w = 1;  // H3D_NLL_W: min waves/SIMD of the NLL-only pass (1, 2, 4)
 };
 
 namespace h3dint {
