@@ -21,9 +21,14 @@ class DispFn(object):
     with knots on integer distances (lowess outputs at the expanded integer
     x), so its tabulation on d = 0..D-1 (``h3d_disp_table``, native) with
     linear interpolation / extrapolation over the integer knots reproduces
-    it. The weighted fit replaces it below ``x[inc_idx]`` by linear
-    interpolation of the raw (distance, dispersion) points, and below the
-    first fitted distance by ``y[0]``; those points are kept here too.
+    it. On top of that, in the reference's order:
+
+    - ``lowess_fit``'s left boundary (``lowess.py:84-85``): every
+      ``x <= left_boundary`` (= the first finite dispersion value,
+      ``analysis.py:212``) returns the fit at its leftmost knot;
+    - the weighted fit then replaces everything below ``x[inc_idx]`` by
+      linear interpolation of the raw (distance, dispersion) points, and below
+      the first fitted distance by ``y[0]`` (``lowess.py:229-242``).
     """
 
     def __init__(self, table, disp_per_dist_col, weighted=True):
@@ -35,18 +40,22 @@ class DispFn(object):
         self.weighted = bool(weighted)
         self.inc_idx = int(np.argmax(np.diff(self.y) > 0) + 1) \
             if self.weighted else 0
+        self.left_boundary = float(self.y[0])
+        # leftmost lowess knot: the first expanded (weighted) or fitted x
+        self.left_value = float(self.table[int(self.x[self.inc_idx])])
 
     def __call__(self, x_star):
         x = np.asarray(x_star, dtype=float)
         t = self.table
-        d = np.arange(len(t), dtype=float)
         xi = np.rint(x)
         on_knot = (xi == x) & (xi >= 0) & (xi < len(t))
         out = np.empty(x.shape, dtype=float)
         out[on_knot] = t[xi[on_knot].astype(np.int64)]
         off = ~on_knot
         if off.any():
-            out[off] = _interp_extrap(d, t, x[off])
+            out[off] = _interp_extrap(np.arange(len(t), dtype=float), t,
+                                      x[off])
+        out[x <= self.left_boundary] = self.left_value
         if self.weighted:
             below = x < self.x[self.inc_idx]
             if below.any():
@@ -72,98 +81,112 @@ class CoreHiC3DeFDR(object):
     def load_bias(self, chrom):
         """Reference ``core.py:35-60``: (n_bins, R); bins failing
         ``bias_thresh`` in any replicate are zeroed."""
-        bias = np.array([np.loadtxt(pattern.replace('<chrom>', chrom))
-                         for pattern in self.bias_patterns]).T
-        bias[(np.any(bias < self.bias_thresh, axis=1)) |
-             (np.any(bias > 1. / self.bias_thresh, axis=1)), :] = 0
+        bias = np.column_stack([np.loadtxt(p.replace('<chrom>', chrom))
+                                for p in self.bias_patterns])
+        lo, hi = self.bias_thresh, 1. / self.bias_thresh
+        bias[((bias < lo) | (bias > hi)).any(axis=1)] = 0
         return bias
+
+    # -- outdir arrays --------------------------------------------------
+    # Which pixel set a per-chromosome stage array is parallel to, as the mask
+    # chain that selects its (row, col) from the union pixel set
+    # (reference core.py:117-134). Stages not listed cannot be loaded as COO.
+    _PIXEL_SET = dict(
+        [(n, ()) for n in ('raw', 'size_factors', 'scaled', 'disp_idx')] +
+        [(n, ('disp_idx',)) for n in ('loop_idx', 'disp', 'mu_hat_null',
+                                      'mu_hat_alt', 'llr', 'pvalues')] +
+        [('qvalues', ('disp_idx', 'loop_idx'))])
+    _NOT_COO = frozenset(['row', 'col', 'bias', 'cov_per_bin',
+                          'disp_per_bin'])
+
+    def _npy(self, name, chrom=None):
+        return '%s/%s.npy' % (self.outdir, name) if chrom is None \
+            else '%s/%s_%s.npy' % (self.outdir, name, chrom)
+
+    def _column(self, rep, cond):
+        """Column of a (pixels, reps) / (pixels, conds) array, or None."""
+        if rep is not None:
+            return list(self.design.index).index(rep)
+        if cond is not None:
+            return list(self.design.columns).index(cond)
+        return None
+
+    @staticmethod
+    def _narrow(mask, sub):
+        """The entries of boolean ``mask`` that ``sub`` (parallel to the True
+        entries of ``mask``) keeps: index chaining (reference core.py:141-145)."""
+        out = np.zeros_like(mask)
+        out[np.flatnonzero(mask)[sub]] = True
+        return out
+
+    @staticmethod
+    def _read(fname, idx, col):
+        """One .npy, optionally subset by a row mask and/or one column."""
+        if idx is None:
+            a = np.load(fname)
+            return a if col is None else a[:, col]
+        a = np.load(fname, mmap_mode='r')
+        return np.asarray(a[idx] if col is None else a[idx, col])
 
     def load_data(self, name, chrom=None, idx=None, rep=None, cond=None,
                   coo=False):
-        """Reference ``core.py:62-196``. Deviation: the reference's
-        ``loop_idx`` short-circuit calls ``np.load_data`` (``core.py:105``, an
-        AttributeError); here it returns the all-True vector it intends."""
-        if name == 'loop_idx' and self.loop_patterns is None and idx is None \
-                and chrom != 'all':
-            disp_idx = self.load_data('disp_idx', chrom)
-            return np.ones(disp_idx.sum(), dtype=bool)
-        col_idx = self.design.index.tolist().index(rep) if rep is not None \
-            else self.design.columns.tolist().index(cond) if cond is not None \
-            else None
+        """Reference ``core.py:62-196``: one chromosome's array (``chrom``),
+        an unchromosomed one (``chrom=None``), or every chromosome
+        concatenated plus offsets (``chrom='all'``; ``idx`` then spans the
+        genome). ``idx`` may be a (big, small) mask pair, chained. ``coo``
+        returns (row, col, data) with row/col taken through the stage's mask
+        chain.
+
+        Deviation: without loop_patterns the reference's ``loop_idx``
+        short-circuit calls the non-existent ``np.load_data``
+        (``core.py:105``); here it returns the all-True vector it intends."""
+        if name == 'loop_idx' and self.loop_patterns is None and \
+                idx is None and chrom != 'all':
+            return np.ones(int(self.load_data('disp_idx', chrom).sum()),
+                           dtype=bool)
+        col = self._column(rep, cond)
         if coo:
             if chrom == 'all' or idx is not None:
                 raise ValueError("cannot pass coo=True with chrom='all' or idx")
-            if name in ['row', 'col', 'bias', 'cov_per_bin', 'disp_per_bin']:
+            if name in self._NOT_COO:
                 raise ValueError('data with name %s cannot be loaded as COO'
                                  % name)
-            if name in ['raw', 'size_factors', 'scaled', 'disp_idx']:
-                row = self.load_data('row', chrom)
-                col = self.load_data('col', chrom)
-            elif name in ['loop_idx', 'disp', 'mu_hat_null', 'mu_hat_alt',
-                          'llr', 'pvalues']:
-                disp_idx = self.load_data('disp_idx', chrom)
-                row = self.load_data('row', chrom, idx=disp_idx)
-                col = self.load_data('col', chrom, idx=disp_idx)
-            elif name in ['qvalues']:
-                disp_idx = self.load_data('disp_idx', chrom)
-                loop_idx = self.load_data('loop_idx', chrom)
-                row = self.load_data('row', chrom, idx=(disp_idx, loop_idx))
-                col = self.load_data('col', chrom, idx=(disp_idx, loop_idx))
-            else:
+            if name not in self._PIXEL_SET:
                 raise ValueError('data name %s not recognized' % name)
+            chain = [self.load_data(m, chrom) for m in self._PIXEL_SET[name]]
+            sel = None
+            if chain:
+                sel = chain[0]
+                for sub in chain[1:]:
+                    sel = self._narrow(sel, sub)
             data = self.load_data(name, chrom)
-            if col_idx is not None:
-                return row, col, data[:, col_idx]
-            return row, col, data
-        if type(idx) == tuple:
-            big_idx, small_idx = idx
-            big_idx = big_idx.copy()
-            big_idx[np.where(big_idx)[0][~small_idx]] = False
-            idx = big_idx
-        if chrom is None:
-            fname = '%s/%s.npy' % (self.outdir, name)
-        elif chrom != 'all':
-            fname = '%s/%s_%s.npy' % (self.outdir, name, chrom)
-        else:
-            fname = None
-        if fname is not None:
-            if idx is None:
-                data = np.load(fname)
-                return data[:, col_idx] if col_idx is not None else data
-            data = np.load(fname, mmap_mode='r')
-            if col_idx is not None:
-                return data[idx, col_idx]
-            return data[idx]
-        idx_offset = 0
-        all_data = []
-        offset = 0
-        offsets = [0]
+            return (self.load_data('row', chrom, idx=sel),
+                    self.load_data('col', chrom, idx=sel),
+                    data if col is None else data[:, col])
+        if isinstance(idx, tuple):
+            idx = self._narrow(*idx)
+        if chrom != 'all':
+            return self._read(self._npy(name, chrom), idx, col)
+        pieces, start = [], 0
         for c in self.chroms:
-            fname = '%s/%s_%s.npy' % (self.outdir, name, c)
+            fname = self._npy(name, c)
+            sub = None
             if idx is not None:
-                data = np.load(fname, mmap_mode='r')
-                full = data.shape[0]
-                data = data[idx[idx_offset:idx_offset + full]]
-                idx_offset += full
-            else:
-                data = np.load(fname)
-            offset += data.shape[0]
-            offsets.append(offset)
-            all_data.append(data)
-        all_data = np.concatenate(all_data)
-        if col_idx is not None:
-            return all_data[:, col_idx], np.array(offsets)
-        return all_data, np.array(offsets)
+                n = np.load(fname, mmap_mode='r').shape[0]
+                sub, start = idx[start:start + n], start + n
+            pieces.append(self._read(fname, sub, col))
+        offsets = np.concatenate([[0], np.cumsum([len(a) for a in pieces])])
+        return np.concatenate(pieces), offsets
 
     def save_data(self, data, name, chrom=None):
-        """Reference ``core.py:198-218``."""
-        if chrom is None:
-            np.save('%s/%s.npy' % (self.outdir, name), data)
-        elif isinstance(chrom, np.ndarray):
-            for i, c in enumerate(self.chroms):
-                self.save_data(data[chrom[i]:chrom[i + 1]], name, c)
-        else:
-            np.save('%s/%s_%s.npy' % (self.outdir, name, chrom), data)
+        """Reference ``core.py:198-218``: ``chrom`` is a chromosome name,
+        None (unchromosomed), or an offsets array splitting ``data`` over
+        ``self.chroms``."""
+        if isinstance(chrom, np.ndarray):
+            for c, lo, hi in zip(self.chroms, chrom[:-1], chrom[1:]):
+                np.save(self._npy(name, c), data[lo:hi])
+            return
+        np.save(self._npy(name, chrom), data)
 
     def load_disp_fn(self, cond):
         """Reference ``core.py:220-236``."""

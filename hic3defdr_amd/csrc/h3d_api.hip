@@ -453,7 +453,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   int64_t* d_lpx = (int64_t*)up("seg_px", lpx.data(), S * 8);
   const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
   int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
-  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len
+  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len, live
   int32_t* d_slb = (int32_t*)scratch(ctx, "seg_lb", S * 4);
   int32_t* d_sle = (int32_t*)scratch(ctx, "seg_le", S * 4);
   double* d_partial = (double*)scratch(ctx, "partial", max_items * 8 * kWavesPerBlock);
@@ -511,14 +511,18 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       ++rounds;
     }
     if (rc) break;
-    if (hipMemcpyAsync(h_meta, d_meta, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(h_meta, d_meta, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(hipGetLastError()));
       break;
     }
     if (std::getenv("H3D_DEBUG"))
-      fprintf(stderr, "[h3d] disp rounds=%d active_items=%d\n", rounds, h_meta[1]);
-    if (h_meta[1] == 0) break;
+      fprintf(stderr, "[h3d] disp rounds=%d active_items=%d live_segments=%d\n", rounds,
+              h_meta[1], h_meta[3]);
+    // terminate on the genome-wide live-segment count (identical on every
+    // rank), not on this rank's own work-list length: a rank without pixels
+    // in the still-active segments must keep joining the collective reduce
+    if (h_meta[3] == 0) break;
     if (rounds > 200000) {
       rc = fail(H3D_ENOCONV, "estimate_disp did not terminate");
       break;

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     const int32_t* __restrict__ seg_chunk_e, int32_t* __restrict__ list,
     int32_t* __restrict__ seg_lb,
     int32_t* __restrict__ seg_le, double* __restrict__ result,
-    int32_t* __restrict__ meta /* [len, active, eq_len] */, int first, int step,
+    int32_t* __restrict__ meta /* [len, active, eq_len, live] */, int first, int step,
     const int64_t* __restrict__ seg_px /* this rank's pixels per segment */,
     unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
   // Every cross-thread step is a wave shuffle tree plus one LDS slot per wave
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(1024) void k_seg_update(
   // round, and the pixel-replicates they visit (measurement: algorithmic bytes
   // of the disp kernels)
   unsigned long long weq = 0ull, wnll = 0ull;
-  int ceq = 0;
+  int ceq = 0, live = 0;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     int phase;
     if (!first && step) {
@@ -385,22 +385,28 @@ __global__ __launch_bounds__(1024) void k_seg_update(
       ceq += seg_chunk_e[s / C] - seg_chunk_b[s / C];
     }
     if (phase == kNll) wnll += w;
+    live += (phase != kDone) ? 1 : 0;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     weq += __shfl_xor(weq, off, 64);
     wnll += __shfl_xor(wnll, off, 64);
     ceq += __shfl_xor(ceq, off, 64);
+    live += __shfl_xor(live, off, 64);
   }
   if (lane == 0) {
     wsum[0][wid] = weq;
     wsum[1][wid] = wnll;
     wscan[0][wid] = ceq;
+    wscan[1][wid] = live;
   }
   __syncthreads();
-  int eq_total = 0;
+  int eq_total = 0, live_total = 0;
 #pragma unroll
-  for (int w = 0; w < kW; ++w) eq_total += wscan[0][w];
+  for (int w = 0; w < kW; ++w) {
+    eq_total += wscan[0][w];
+    live_total += wscan[1][w];
+  }
   if (threadIdx.x == 0) {
     unsigned long long a = 0ull, b = 0ull;
     for (int w = 0; w < kW; ++w) {
@@ -467,6 +473,11 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     meta[0] = base_nll;
     meta[1] = base_nll;
     meta[2] = eq_total;
+    // segments not yet kDone, genome-wide: with a cross-rank reduce every
+    // rank steps identical state machines, so this count (unlike this
+    // rank's own list length meta[1]) is the same on every rank and is what
+    // the host loop terminates on
+    meta[3] = live_total;
   }
 }
 

@@ -65,6 +65,12 @@ E2E = {
     # name: (chrom sizes, dist_thresh_max, n_per_cond, seed, use loops)
     'small2': ({'chrA': 420, 'chrB': 300}, 50, (2, 2), 0, True),
     'c3r9': ({'chrC': 260}, 40, (3, 3, 3), 1, False),
+    # cfg4's shape at fixture size: 6 replicates x 3 conditions (R = 18:
+    # k_lrt<32, 8>, the M = 8 disp path, chi2 df = 2)
+    'r18c3': ({'chrD': 220}, 60, (6, 6, 6), 2, False),
+    # >= 8 replicates in a condition: numpy's pairwise row sums
+    # (np_sum n >= 8 branch, the k_disp_work nr >= 8 path, k_lrt<16, 2>)
+    'r16c2': ({'chrE': 200}, 40, (8, 8), 3, False),
 }
 
 
@@ -389,9 +395,214 @@ def run_alternatives(name='small2'):
     print('alternatives', name, sorted(out))
 
 
+class _PerRepFactors(np.ndarray):
+    """Size factors of a non-conditional norm, shape (R,). The reference's
+    estimate_disp indexes them with the pixel mask
+    (``analysis.py:181``: ``size_factors[disp_idx_chrom]``), which raises for
+    a 1-D array; its lrt broadcasts them (``analysis.py:274-275``). Fixture
+    generation pins the evident intent: a pixel mask returns the per-replicate
+    vector unchanged, so ``f`` broadcasts exactly as in lrt."""
+
+    def __getitem__(self, key):
+        k = np.asarray(key) if not isinstance(key, tuple) else None
+        if k is not None and k.dtype == bool and k.shape != self.shape:
+            return np.asarray(self)
+        return super().__getitem__(key)
+
+
+NORMS = ['conditional_scaling', 'median_of_ratios', 'simple_scaling',
+         'no_scaling']
+
+
+def run_norms(name='small2'):
+    """run_to_qvalues on the small2 inputs with every non-default norm
+    (scaling.py:10-65, 130-149; dispatched at analysis.py:104-108):
+    norm_<name>.npz holds <norm>__<stage>__<chrom> for every outdir array.
+    For the per-replicate (1-D) norms the estimate_disp indexing patch of
+    _PerRepFactors is applied (meta_sf1d_patch)."""
+    sizes, dmax, npc, seed, loops = E2E[name]
+    base = os.path.join(HERE, 'data', name)
+    g = np.load(os.path.join(HERE, 'e2e_%s.npz' % name))
+    reps = [str(r) for r in g['meta_reps']]
+    conds = [str(c) for c in g['meta_conds']]
+    chroms = [str(c) for c in g['meta_chroms']]
+    design = pd.DataFrame(g['meta_design'].astype(bool), index=reps,
+                          columns=conds)
+    lp = {c: os.path.join(base, 'clusters', '%s_<chrom>.json' % c)
+          for c in conds} if loops else None
+    out = {'meta_norms': np.array(NORMS), 'meta_sf1d_patch': np.array(True)}
+    for norm in NORMS:
+        outdir = os.path.join('/tmp', 'h3golden_norm_%s_%s' % (norm, name))
+        shutil.rmtree(outdir, ignore_errors=True)
+        h = HiC3DeFDR(raw_npz_patterns=[os.path.join(base, r, '<chrom>_raw.npz')
+                                        for r in reps],
+                      bias_patterns=[os.path.join(base, r, '<chrom>_kr.bias')
+                                     for r in reps],
+                      chroms=chroms, design=design, outdir=outdir,
+                      dist_thresh_max=dmax, loop_patterns=lp)
+        plain = h.load_data
+
+        def patched(nm, *a, **k):
+            v = plain(nm, *a, **k)
+            if nm == 'size_factors' and isinstance(v, np.ndarray) and \
+                    v.ndim == 1:
+                v = v.view(_PerRepFactors)
+            return v
+        h.load_data = patched
+        h.run_to_qvalues(norm=norm, n_threads=0, verbose=False)
+        for chrom in chroms:
+            for st in STAGES:
+                fn = os.path.join(outdir, '%s_%s.npy' % (st, chrom))
+                if os.path.exists(fn):
+                    out['%s__%s__%s' % (norm, st, chrom)] = np.load(fn)
+        out['%s__disp_per_dist' % norm] = np.load(
+            os.path.join(outdir, 'disp_per_dist.npy'))
+    np.savez_compressed(os.path.join(HERE, 'norm_%s.npz' % name), **out)
+    print('norms', name, len(out))
+
+
+def _lowess_floor_drops(col):
+    """True when the reference's weighted lowess (lowess.py:172-201) floors
+    some scaled weight to 0 -- ``weight * (1 / min_weight)`` rounding to
+    1 - 2**-53 at the least precise distance -- and silently drops that
+    distance from the fit."""
+    fin = np.isfinite(col)
+    y = col[fin]
+    var = pd.Series(y).rolling(window=20, center=True).var().values
+    prec = 1 / var
+    w = np.full(len(y), np.nan)
+    w[np.isfinite(prec)] = np.power(prec[np.isfinite(prec)], 0.25)
+    sw = w * (1 / np.nanmin(w))
+    return bool(np.any(np.floor(sw[np.isfinite(sw)]) == 0))
+
+
+def run_lowess_drop(max_tries=60):
+    """A dataset on which the reference's weighted-lowess floor drop fires
+    for at least one condition, run to q-values and thresholded
+    (e2e_lwdrop.npz + calls in the same file). Used to measure what the
+    product's pinned deviation (minimum scaled weight exactly 1) costs in
+    q-values and calls."""
+    dmax = 60
+    for seed in range(100, 100 + max_tries):
+        base = os.path.join(HERE, 'data', 'lwdrop')
+        shutil.rmtree(base, ignore_errors=True)
+        kw = synthetic.write_dataset(base, {'chrL': 240}, dist_thresh_max=dmax,
+                                     seed=seed, clusters_per_chrom=10)
+        design = pd.DataFrame(kw['design'], index=kw['reps'],
+                              columns=kw['conds'])
+        outdir = os.path.join('/tmp', 'h3golden_out_lwdrop')
+        shutil.rmtree(outdir, ignore_errors=True)
+        h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                      bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                      design=design, outdir=outdir, dist_thresh_max=dmax,
+                      loop_patterns=kw['loop_patterns'], res=10000)
+        h.prepare_data(n_threads=0, verbose=False)
+        h.estimate_disp(n_threads=0)
+        dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
+        fires = [_lowess_floor_drops(dpd[:, c]) for c in range(dpd.shape[1])]
+        if not any(fires):
+            continue
+        h.lrt(n_threads=0, verbose=False)
+        h.bh()
+        out = {'meta_equal_bin': np.array('stable'),
+               'meta_chroms': np.array(kw['chroms']),
+               'meta_reps': np.array(kw['reps']),
+               'meta_conds': np.array(kw['conds']),
+               'meta_design': kw['design'],
+               'meta_dist_thresh_max': np.array(dmax),
+               'meta_loops': np.array(True), 'meta_seed': np.array(seed),
+               'meta_floor_drop': np.array(fires)}
+        for chrom in kw['chroms']:
+            for st in STAGES:
+                fn = os.path.join(outdir, '%s_%s.npy' % (st, chrom))
+                if os.path.exists(fn):
+                    out['%s__%s' % (st, chrom)] = np.load(fn)
+        out['disp_per_dist'] = dpd
+        for c, cond in enumerate(kw['conds']):
+            out['disp_fn_table__%s' % cond] = h.load_disp_fn(cond)(
+                np.arange(dmax + 1))
+        np.savez_compressed(os.path.join(HERE, 'e2e_lwdrop.npz'), **out)
+        print('lwdrop seed', seed, 'fires', fires)
+        return
+    raise RuntimeError('no floor drop in %d seeds' % max_tries)
+
+
+def run_hard_cfg2(bins=20000, dmax=250, seed=0):
+    """The pixels of the headline workload (bench.py cfg2: one synthetic
+    chromosome of 20k bins, seed 0, dmax 250) on which the reference's array
+    secant fails for any of the lrt's 1 + C mean fits (scaled_nb.py:155-160),
+    i.e. the pixels its brentq fallback (:162-181) solves. The reference's
+    prepare_data + estimate_disp run on the whole chromosome (their disp is
+    what lrt sees); the secant-failure set is found with the CPU restatement
+    (oracle/restatement.py _array_secant, same iteration as scipy 1.7.1);
+    the reference's lrt then runs on just those pixels (O(fail * N) is small
+    at N = fail). hard_cfg2.npz: raw, f, disp (per pixel, wide), design and
+    the reference's p, llr, mu0, mu1."""
+    sys.path.insert(0, REPO)
+    from oracle import restatement as orc
+    from hic3defdr.util import lrt as lrt_mod
+    base = os.path.join('/tmp', 'h3golden_cfg2_data')
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, {'chrB0': bins}, dist_thresh_max=dmax,
+                                 seed=seed)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_cfg2_out')
+    shutil.rmtree(outdir, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax)
+    h.prepare_data(n_threads=-1, verbose=False)
+    h.estimate_disp(n_threads=-1)
+    chrom = kw['chroms'][0]
+    bias = h.load_bias(chrom)
+    sf = h.load_data('size_factors', chrom)
+    di = h.load_data('disp_idx', chrom)
+    row = h.load_data('row', chrom, idx=di)
+    col = h.load_data('col', chrom, idx=di)
+    raw = h.load_data('raw', chrom, idx=di)
+    disp = h.load_data('disp', chrom)
+    f = bias[row] * bias[col] * sf[di, :]
+    dw = np.dot(disp, design.values.T)
+    dsg = design.values
+    failed = np.zeros(len(raw), dtype=bool)
+    fits = [np.ones(dsg.shape[0], dtype=bool)] + \
+        [dsg[:, c] for c in range(dsg.shape[1])]
+    for m in fits:
+        x, b, a = raw[:, m], f[:, m], dw[:, m]
+
+        def fn(mu):
+            return np.sum((x - mu[:, None] * b) /
+                          (mu[:, None] + a * mu[:, None] ** 2 * b), axis=-1)
+        root, conv, zder = orc._array_secant(fn, np.mean(x / b, axis=1))
+        bad = ~conv | zder | (root <= 0) | \
+            (root >= np.sqrt(np.finfo(float).max) / 1e10)
+        with np.errstate(all='ignore'):
+            bad |= ~np.isclose(fn(root), 0, atol=1e-5)
+        failed |= bad
+    idx = np.where(failed)[0]
+    print('cfg2 disp pixels', len(raw), 'secant failures', len(idx))
+    p, llr, m0, m1 = lrt_mod.lrt(raw[idx], f[idx], dw[idx], dsg)
+    np.savez_compressed(os.path.join(HERE, 'hard_cfg2.npz'),
+                        raw=raw[idx], f=f[idx], disp=disp[idx],
+                        dist=(col - row)[idx], design=dsg, p=p, llr=llr,
+                        mu0=m0, mu1=m1, n_disp_pixels=np.array(len(raw)),
+                        meta_bins=np.array(bins), meta_dmax=np.array(dmax),
+                        meta_seed=np.array(seed))
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling',
-                             'calls', 'clusters', 'alt']
+                             'calls', 'clusters', 'alt', 'norms', 'lwdrop',
+                             'hard_cfg2']
+    for w in which:
+        if w.startswith('e2e:'):
+            run_e2e(w[4:])
+    if 'norms' in which:
+        run_norms('small2')
+    if 'lwdrop' in which:
+        run_lowess_drop()
+    if 'hard_cfg2' in which:
+        run_hard_cfg2()
     if 'alt' in which:
         run_alternatives('small2')
     if 'calls' in which:
