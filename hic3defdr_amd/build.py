@@ -1,13 +1,23 @@
 """In-tree build of the native libraries (no cmake; plain hipcc / g++).
 
 - ``libh3d.so``          the product: C-ABI host code + gfx950 HIP kernels
-                          (csrc/h3d_api.hip), loaded by hic3defdr_amd._native.
+                          (csrc/h3d_api.hip, h3d_alt.hip, h3d_calls.cpp), loaded
+                          by hic3defdr_amd._native.
 - ``libh3d_hosttest.so`` the device numerics compiled for the host, used only
                           by CPU unit tests (tests/test_special_host.py).
+- ``libh3d_selftest.so`` the same numerics compiled for gfx950 behind the same
+                          test ABI, used only by GPU unit tests.
 
-Both land in ``hic3defdr_amd/lib/`` so they travel to the GPU box with the
+All land in ``hic3defdr_amd/lib/`` so they travel to the GPU box with the
 repo snapshot (they are git-ignored, not gpurun-ignored).
+
+Staleness is decided by CONTENT, not mtimes: every output carries a
+``.stamp`` file holding the sha256 of its compile command and of every source
+and header it is built from, and is rebuilt whenever that digest changes. A
+binary copied from another tree (or a stale one whose sources were edited
+with an older mtime) is therefore never silently reused.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -15,70 +25,99 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIBDIR = os.path.join(PKG, 'lib')
+INC = os.path.join(os.path.dirname(PKG), 'include')
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 
-# (source, compiler): device TU through hipcc, host-only TUs through g++
+# (source, compiler): device TUs through hipcc, host-only TUs through g++
 NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
                ('h3d_calls.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
            'h3d_prepare.h', 'h3d_prepare_api.h', 'h3d_errors.h',
-           'h3d_ctx.h']
+           'h3d_ctx.h', 'h3d_norms.h']
+HIP_FLAGS = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC',
+             '-munsafe-fp-atomics']
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+def _digest(cmd, deps):
+    h = hashlib.sha256(' '.join(cmd).encode())
+    for d in sorted(deps):
+        if os.path.exists(d):
+            h.update(d.encode())
+            with open(d, 'rb') as fh:
+                h.update(fh.read())
+    return h.hexdigest()
 
 
-def _run(cmd):
+def _fresh(target, digest):
+    try:
+        with open(target + '.stamp') as fh:
+            return os.path.exists(target) and fh.read().strip() == digest
+    except OSError:
+        return False
+
+
+def _run(cmd, target, digest):
     print('[h3d build]', ' '.join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
+    with open(target + '.stamp', 'w') as fh:
+        fh.write(digest + '\n')
+
+
+def _build(target, cmd, deps, force):
+    dig = _digest(cmd, deps)
+    if force or not _fresh(target, dig):
+        _run(cmd, target, dig)
+    return target
+
+
+def _headers():
+    return [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(INC, 'h3d.h')]
 
 
 def build_hosttest(force=False):
     os.makedirs(LIBDIR, exist_ok=True)
     out = os.path.join(LIBDIR, 'libh3d_hosttest.so')
     src = os.path.join(CSRC, 'h3d_hosttest.cpp')
-    deps = [src] + [os.path.join(CSRC, h) for h in HEADERS]
-    if force or _stale(out, deps):
-        _run(['g++', '-O2', '-std=c++17', '-shared', '-fPIC',
-              '-ffp-contract=off', '-o', out, src])
-    return out
+    cmd = ['g++', '-O2', '-std=c++17', '-shared', '-fPIC',
+           '-ffp-contract=off', '-o', out, src]
+    return _build(out, cmd, [src] + _headers(), force)
+
+
+def build_selftest(force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, 'libh3d_selftest.so')
+    src = os.path.join(CSRC, 'h3d_selftest.hip')
+    cmd = [HIPCC] + HIP_FLAGS + ['-shared', '-o', out, src]
+    return _build(out, cmd, [src] + _headers(), force)
 
 
 def build_native(force=False):
-    """Compiles each TU to an object (rebuilt only when it or a header is
-    newer), then links libh3d.so with hipcc."""
+    """Compiles each TU to an object, then links libh3d.so with hipcc; each
+    step is skipped when its content digest is unchanged."""
     os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
     out = os.path.join(LIBDIR, 'libh3d.so')
-    inc = os.path.join(os.path.dirname(PKG), 'include')
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + \
-        [os.path.join(inc, 'h3d.h')]
+    hdrs = _headers()
     objs = []
     for src, cc in NATIVE_SRCS:
         s = os.path.join(CSRC, src)
         o = os.path.join(LIBDIR, 'obj', src + '.o')
         objs.append(o)
-        if force or _stale(o, [s] + hdrs):
-            if cc == 'hipcc':
-                _run([HIPCC, '--offload-arch=%s' % ARCH, '-O3', '-std=c++17',
-                      '-fPIC', '-munsafe-fp-atomics', '-I', inc, '-c', '-o', o,
-                      s])
-            else:
-                _run(['g++', '-O2', '-std=c++17', '-fPIC', '-I', inc, '-c',
-                      '-o', o, s])
-    if force or _stale(out, objs):
-        _run([HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out]
-             + objs)
-    return out
+        if cc == 'hipcc':
+            cmd = [HIPCC] + HIP_FLAGS + ['-I', INC, '-c', '-o', o, s]
+        else:
+            cmd = ['g++', '-O2', '-std=c++17', '-fPIC', '-I', INC, '-c', '-o',
+                   o, s]
+        _build(o, cmd, [s] + hdrs, force)
+    cmd = [HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out] \
+        + objs
+    return _build(out, cmd, objs, force)
 
 
 def build_all(force=False):
-    return build_native(force), build_hosttest(force)
+    return build_native(force), build_hosttest(force), build_selftest(force)
 
 
 if __name__ == '__main__':

@@ -452,6 +452,8 @@ def run_norms(name='small2'):
         h.run_to_qvalues(norm=norm, n_threads=0, verbose=False)
         for chrom in chroms:
             for st in STAGES:
+                if st in ('row', 'col', 'raw', 'scaled'):
+                    continue  # norm-independent / derived (= balanced / sf)
                 fn = os.path.join(outdir, '%s_%s.npy' % (st, chrom))
                 if os.path.exists(fn):
                     out['%s__%s__%s' % (norm, st, chrom)] = np.load(fn)

@@ -54,7 +54,7 @@ def test_disp_table_matches_reference_lowess_goldens(lib):
         assert rel_err(tab2, g['ul%d_table' % t]) < 1e-12
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3'])
 def test_disp_table_matches_e2e_disp_fn(lib, name):
     g, kw = e2e_inputs(name)
     for c, cond in enumerate(kw['conds']):
@@ -62,7 +62,7 @@ def test_disp_table_matches_e2e_disp_fn(lib, name):
         assert rel_err(tab, g['disp_fn_table__%s' % cond]) < 1e-12
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3'])
 def test_pickled_disp_fn_matches_reference_closure(lib, name):
     """DispFn (the product's picklable disp_fn) vs the reference's lowess
     closure evaluated at non-integer, negative and beyond-range distances."""

@@ -27,7 +27,35 @@ def _run(name, outdir):
     return g, kw, h
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+# Fixtures on which the reference's weighted lowess floors a scaled weight to
+# 0 and drops a distance from the fit (lowess.py:183-201; DESIGN.md §3 item
+# 2): the product's pinned deviation (minimum scaled weight exactly 1, shared
+# by the oracle) moves the smoothed dispersion there, so downstream arrays
+# are held to the oracle at the north-star bar and to the reference at the
+# measured bound below.
+FLOOR_DROP = {'r16c2', 'lwdrop'}
+DROP_MAX_ABS_DQ = 0.02        # measured: 3.2e-3 (r16c2), 9.6e-3 (lwdrop)
+DROP_STRICT_FDRS = (0.01, 0.05)
+
+
+def _oracle_run(kw):
+    import oracle
+    chroms = kw['chroms']
+    npz = {c: [p.replace('<chrom>', c) for p in kw['raw_npz_patterns']]
+           for c in chroms}
+    bias = {c: [p.replace('<chrom>', c) for p in kw['bias_patterns']]
+            for c in chroms}
+    loops = None
+    if kw['loop_patterns']:
+        loops = {c: [p.replace('<chrom>', c)
+                     for p in kw['loop_patterns'].values()] for c in chroms}
+    return oracle.run_to_qvalues(npz, bias, chroms, kw['design'],
+                                 dist_thresh_max=kw['dist_thresh_max'],
+                                 loop_files=loops)
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3', 'r16c2',
+                                  'lwdrop'])
 def test_run_to_qvalues_matches_reference(name):
     outdir = tempfile.mkdtemp(prefix='h3d_e2e_')
     try:
@@ -35,6 +63,8 @@ def test_run_to_qvalues_matches_reference(name):
         dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
         np.testing.assert_array_equal(np.isnan(dpd), np.isnan(g['disp_per_dist']))
         np.testing.assert_allclose(dpd, g['disp_per_dist'], rtol=1e-6, atol=1e-12)
+        drop = name in FLOOR_DROP
+        orc = _oracle_run(kw) if drop else None
         for c in kw['chroms']:
             ld = lambda st: np.load(os.path.join(outdir, '%s_%s.npy' % (st, c)))
             for st in ('row', 'col', 'raw', 'disp_idx'):   # bit-exact
@@ -45,6 +75,18 @@ def test_run_to_qvalues_matches_reference(name):
                 np.testing.assert_array_equal(ld('loop_idx'), g['loop_idx__%s' % c])
             assert rel_err(ld('size_factors'), g['size_factors__%s' % c]) < 1e-13
             assert rel_err(ld('scaled'), g['scaled__%s' % c]) < 1e-13
+            if drop:
+                # north-star bar against the oracle (same pinned lowess)
+                for st in ('disp', 'pvalues', 'qvalues'):
+                    assert rel_err(ld(st), orc[c][st]) < 1e-6, st
+                for st in ('mu_hat_null', 'mu_hat_alt'):
+                    assert rel_err(ld(st), orc[c][st]) < 1e-8, st
+                # measured bound against the reference
+                q, qr = ld('qvalues'), g['qvalues__%s' % c]
+                assert np.nanmax(np.abs(q - qr)) < DROP_MAX_ABS_DQ
+                for fdr in DROP_STRICT_FDRS:
+                    np.testing.assert_array_equal(q < fdr, qr < fdr)
+                continue
             assert rel_err(ld('disp'), g['disp__%s' % c]) < 1e-6
             assert rel_err(ld('pvalues'), g['pvalues__%s' % c]) < 1e-6
             assert rel_err(ld('qvalues'), g['qvalues__%s' % c]) < 1e-6
@@ -58,20 +100,23 @@ def test_run_to_qvalues_matches_reference(name):
         from hic3defdr_amd import HiC3DeFDR
         h2 = HiC3DeFDR.load(outdir)
         assert h2.chroms == kw['chroms']
-        xs = g['disp_fn_xs']
-        for cond in kw['conds']:
-            fn = h2.load_disp_fn(cond)
-            assert rel_err(fn(xs), g['disp_fn_cont__%s' % cond]) < 1e-6
+        if 'disp_fn_xs' in g and not drop:
+            xs = g['disp_fn_xs']
+            for cond in kw['conds']:
+                fn = h2.load_disp_fn(cond)
+                assert rel_err(fn(xs), g['disp_fn_cont__%s' % cond]) < 1e-6
         q_all, off = h2.load_data('qvalues', 'all')
         assert off[-1] == len(q_all)
         r, cc, v = h2.load_data('qvalues', kw['chroms'][0], coo=True)
         assert len(r) == len(cc) == len(v)
         # downstream calls on the GPU q-values: same clusters, same tables
         # as the reference (threshold -> classify -> collect)
-        from test_calls import assert_calls_match
-        ref = golden('calls_%s.npz' % name)
-        h2.collect(fdr=[float(x) for x in ref['meta_fdrs']],
-                   cluster_size=[int(x) for x in ref['meta_sizes']])
-        assert_calls_match(outdir, name)
+        if os.path.exists(os.path.join(os.path.dirname(__file__), 'golden',
+                                       'calls_%s.npz' % name)):
+            from test_calls import assert_calls_match
+            ref = golden('calls_%s.npz' % name)
+            h2.collect(fdr=[float(x) for x in ref['meta_fdrs']],
+                       cluster_size=[int(x) for x in ref['meta_sizes']])
+            assert_calls_match(outdir, name)
     finally:
         shutil.rmtree(outdir, ignore_errors=True)

@@ -38,7 +38,7 @@ def _stage_inputs(name):
         np.concatenate(dists)
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3', 'r16c2'])
 def test_disp_per_dist_vs_reference(ctx, name):
     g, kw, raw, f, dist = _stage_inputs(name)
     design = kw['design']
@@ -50,13 +50,15 @@ def test_disp_per_dist_vs_reference(ctx, name):
     np.testing.assert_allclose(out, ref, rtol=RTOL_DISP, atol=1e-12)
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3', 'r16c2'])
 def test_lrt_vs_reference(ctx, name):
     from hic3defdr_amd import _native
     g, kw, raw, f, dist = _stage_inputs(name)
     design = kw['design']
-    tab = np.stack([_native.disp_table(g['disp_per_dist'][:, c])
-                    for c in range(design.shape[1])], axis=1)
+    # the reference's own fitted table (disp_fn at every integer distance),
+    # so this checks the LRT alone (the smoother is checked in test_abi)
+    tab = np.stack([g['disp_fn_table__%s' % cond] for cond in kw['conds']],
+                   axis=1)
     p, llr, m0, m1, disp = ctx.lrt(raw, f, dist, tab, design.argmax(axis=1))
     pr = np.concatenate([g['pvalues__%s' % c] for c in kw['chroms']])
     m0r = np.concatenate([g['mu_hat_null__%s' % c] for c in kw['chroms']])
@@ -84,7 +86,7 @@ def test_lrt_refit_false_vs_oracle(ctx):
     assert rel_err(m1, rm1) < 1e-14
 
 
-@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3', 'r16c2'])
 def test_union_and_size_factors_vs_reference(ctx, name):
     g, kw = e2e_inputs(name)
     for c in kw['chroms']:
@@ -136,3 +138,34 @@ def test_disp_and_lrt_vs_oracle_larger(ctx):
         rp, _, rm0, rm1 = oracle.lrt(raw, f, np.dot(disp, design.T), design)
         assert rel_err(p, rp) < RTOL_PQ
         assert rel_err(m0, rm0) < RTOL_MU
+
+
+def test_disp_dev_with_noop_reduce_matches_single_rank(ctx):
+    """The multi-rank branch of the device driver (k_seg_reduce without the
+    state step, k_seg_update step=1, the reduce hook on the ctx stream,
+    termination on the live-segment count) with an identity all-reduce gives
+    the single-rank result bit for bit."""
+    import torch
+    from hic3defdr_amd import _native
+    g, kw, raw, f, dist = _stage_inputs('small2')
+    design = kw['design']
+    C, D = design.shape[1], kw['dist_thresh_max'] + 1
+    cond = design.argmax(axis=1)
+    dev = torch.device('cuda', 0)
+    t_raw = torch.from_numpy(raw.astype(np.int32)).to(dev).contiguous()
+    t_f = torch.from_numpy(f).to(dev).contiguous()
+    t_d = torch.from_numpy(dist.astype(np.int32)).to(dev).contiguous()
+    torch.cuda.synchronize()
+    calls = []
+
+    def noop(ptr, count):
+        calls.append(count)
+
+    args = (t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
+            raw.shape[1], cond, C, D)
+    one = ctx.disp_per_dist_dev(*args)
+    multi = ctx.disp_per_dist_dev(*args, reduce=noop)
+    assert len(calls) > 10
+    np.testing.assert_array_equal(one, multi)
+    np.testing.assert_allclose(multi, g['disp_per_dist'], rtol=RTOL_DISP,
+                               atol=1e-12)

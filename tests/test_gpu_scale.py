@@ -1,0 +1,90 @@
+"""The headline workload (BASELINE.json configs[1], cfg2: one synthetic
+chromosome of 20k bins, R = 4, dist_thresh_max 250) on the GPU:
+
+- the pixels on which the reference's array secant fails (the ones its
+  O(fail * N) brentq fallback solves, scaled_nb.py:162-181) are held to the
+  reference's own lrt on them (tests/golden/hard_cfg2.npz, made by
+  tests/golden/make_golden.py run_hard_cfg2);
+- the whole chromosome through prepare_data -> estimate_disp -> lrt is held
+  to size-independent properties: no status flags, p in [0, 1], no NaN
+  outside empty segments, and bit-identical results on a second call.
+"""
+import os
+import shutil
+import tempfile
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+
+RTOL_PQ = 1e-6
+RTOL_MU = 1e-8
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from hic3defdr_amd import _native
+    return _native.context(0)
+
+
+def test_cfg2_secant_failure_pixels_vs_reference(ctx):
+    g = golden('hard_cfg2.npz')
+    design = g['design'].astype(bool)
+    cond = design.argmax(axis=1)
+    # per-pixel dispersions (the reference's disp for these pixels)
+    p, llr, m0, m1, _ = ctx.lrt(g['raw'], g['f'], None, g['disp'], cond,
+                                want_disp=False)
+    assert len(p) == 2975
+    assert rel_err(p, g['p']) < RTOL_PQ
+    assert rel_err(m0, g['mu0']) < RTOL_MU
+    assert rel_err(m1, g['mu1']) < RTOL_MU
+    # the llr itself: absolute, it crosses zero
+    assert np.max(np.abs(llr - g['llr'])) < 1e-8
+
+
+@pytest.fixture(scope='module')
+def cfg2(ctx):
+    from hic3defdr_amd import HiC3DeFDR, synthetic
+    tmp = tempfile.mkdtemp(prefix='h3d_cfg2_')
+    try:
+        kw = synthetic.write_dataset(tmp, {'chrB0': 20000},
+                                     dist_thresh_max=250, seed=0)
+        design = pd.DataFrame(kw['design'], index=kw['reps'],
+                              columns=kw['conds'])
+        h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                      bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                      design=design, outdir=os.path.join(tmp, 'out'),
+                      dist_thresh_max=250)
+        h.prepare_data(verbose=False)
+        raw, f, dist, _ = h._f_and_dist()
+        yield raw, f, dist, kw['design']
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_cfg2_full_size_properties(ctx, cfg2):
+    from hic3defdr_amd import _native
+    raw, f, dist, design = cfg2
+    assert len(raw) == int(golden('hard_cfg2.npz')['n_disp_pixels'])
+    cond = design.argmax(axis=1)
+    C, D = design.shape[1], 251
+    runs = []
+    for _ in range(2):
+        dpd = ctx.disp_per_dist(raw, f, dist, cond, C, D)   # raises on flags
+        tab = _native.disp_tables(dpd)
+        runs.append((dpd,) + ctx.lrt(raw, f, dist, tab, cond))
+    dpd, p, llr, m0, m1, disp = runs[0]
+    present = np.isin(np.arange(D), dist)
+    assert np.all(np.isfinite(dpd[present]))
+    assert np.all(np.isnan(dpd[~present]))
+    assert np.all((dpd[present] > 0) & (dpd[present] < 100.0))
+    assert np.all(np.isfinite(p)) and np.all((p >= 0) & (p <= 1))
+    assert np.all(np.isfinite(m0)) and np.all(m0 > 0)
+    assert np.all(np.isfinite(m1)) and np.all(m1 > 0)
+    assert np.all(llr <= 1e-9)   # the null is nested in the alternative
+    for a, b in zip(runs[0], runs[1]):   # deterministic: bit-identical
+        np.testing.assert_array_equal(a, b)

@@ -1,7 +1,16 @@
-"""Host build of the device numerics (csrc/h3d_special.h, h3d_model.h) vs
-scipy / the oracle / reference goldens. CPU only: the same source the gfx950
-kernels compile, built with g++ (libh3d_hosttest.so)."""
+"""The device numerics (csrc/h3d_special.h, h3d_model.h) vs scipy / the
+oracle / reference goldens, through two builds of the same source behind one
+test ABI (h3dt_*):
+
+- ``host``:   g++ (libh3d_hosttest.so), runs on the CPU;
+- ``gfx950``: hipcc for gfx950 (libh3d_selftest.so, csrc/h3d_selftest.hip):
+  every call runs the device code in a kernel on the MI355X -- OCML
+  exp/log, the contracted NLL lgamma -- so the unit goldens hold the
+  kernels' own numerics (marked gpu).
+
+Same tolerances for both."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -16,9 +25,18 @@ D = ctypes.POINTER(ctypes.c_double)
 I = ctypes.POINTER(ctypes.c_int32)
 
 
-@pytest.fixture(scope='module')
-def lib():
-    return ctypes.CDLL(h3dbuild.build_hosttest())
+@pytest.fixture(scope='module',
+                params=['host', pytest.param('gfx950', marks=pytest.mark.gpu)])
+def lib(request):
+    if request.param == 'host':
+        return ctypes.CDLL(h3dbuild.build_hosttest())
+    # prebuilt in-tree by build() (the GPU box does not compile)
+    path = os.path.join(h3dbuild.LIBDIR, 'libh3d_selftest.so')
+    if not os.path.exists(path):
+        raise RuntimeError('libh3d_selftest.so missing: run build()')
+    lib = ctypes.CDLL(path)
+    assert lib.h3dt_device_ok() == 1, 'no HIP device for the gfx950 self-test'
+    return lib
 
 
 def _p(a, t=D):
