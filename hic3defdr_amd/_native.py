@@ -13,6 +13,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('H3D_LIB', os.path.join(PKG, 'lib', 'libh3d.so'))
 
 H3D_EST = {'qcml': 0, 'cml': 1, 'mme': 2}
+# size-factor methods (util/scaling.py), h3d.h H3D_NORM_*
+H3D_NORM = {'conditional_mor': 0, 'conditional_scaling': 1,
+            'median_of_ratios': 2, 'simple_scaling': 3, 'no_scaling': 4}
 
 ERRORS = {-1: 'bad argument', -2: 'HIP runtime error',
           -3: 'numerical failure', -4: 'out of device memory',
@@ -21,7 +24,7 @@ ERRORS = {-1: 'bad argument', -2: 'HIP runtime error',
 EXPORTS = [
     'h3d_version', 'h3d_device_count', 'h3d_open', 'h3d_close',
     'h3d_last_error', 'h3d_set_stream', 'h3d_union_count', 'h3d_union_fill',
-    'h3d_size_factors_cmor', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
+    'h3d_size_factors_cmor', 'h3d_size_factors', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
     'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
@@ -66,6 +69,7 @@ def load_library(path=None):
             'h3d_union_count': (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
             'h3d_union_fill': (_I, [_P, _P, _P, _P, _P, _I64]),
             'h3d_size_factors_cmor': (_I, [_P, _P, _P, _I64, _I, _I, _P]),
+            'h3d_size_factors': (_I, [_P, _P, _P, _I64, _I, _I, _I, _P]),
             'h3d_disp_per_dist': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I,
                                        _I, _P, _P]),
             'h3d_disp_per_dist_dev': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P,
@@ -182,6 +186,22 @@ class Context(object):
         _check(self.lib.h3d_size_factors_cmor(
             self.handle, _ptr(balanced), _ptr(dist), n, R,
             int(n_bins or 0), _ptr(out)), 'h3d_size_factors_cmor')
+        return out
+
+    def size_factors(self, balanced, dist, norm='conditional_mor', n_bins=0):
+        """Any norm of util/scaling.py: the conditional ones give (n, R)
+        (``n_bins`` equal-number distance bins, 0/None = exact distances),
+        the others (R,)."""
+        if norm not in H3D_NORM:
+            raise ValueError('unknown norm %r' % (norm,))
+        balanced = _c(balanced, np.float64)
+        n, R = balanced.shape
+        cond = norm.startswith('conditional')
+        dist = _c(dist, np.int32) if cond else None
+        out = np.empty((n, R) if cond else R, dtype=np.float64)
+        _check(self.lib.h3d_size_factors(
+            self.handle, _ptr(balanced), _ptr(dist), n, R, H3D_NORM[norm],
+            int(n_bins or 0), _ptr(out)), 'h3d_size_factors')
         return out
 
     # -- estimate_disp ------------------------------------------------------

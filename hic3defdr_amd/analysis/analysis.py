@@ -4,7 +4,7 @@ Same methods, signatures and outdir outputs as the reference; the per-pixel
 work runs on the GPU through libh3d.so:
 
   prepare_data  -> h3d_union_count/fill (union + raw/balanced gathers),
-                   h3d_size_factors_cmor (conditional median of ratios)
+                   h3d_size_factors (every norm of util/scaling.py)
   estimate_disp -> h3d_disp_per_dist (qcml per distance x condition),
                    h3d_disp_table (lowess smoother, host C++ in libh3d)
   lrt           -> h3d_lrt (fused per-pixel NB GLM fits + LRT + chi2)
@@ -32,7 +32,7 @@ from hic3defdr_amd.util.clusters import (load_clusters, load_cluster_list,
 from hic3defdr_amd.util.thresholding import threshold_clusters
 from hic3defdr_amd.util.printing import eprint
 
-NATIVE_NORMS = ('conditional_mor',)
+NATIVE_NORMS = tuple(_native.H3D_NORM)
 NATIVE_ESTIMATORS = ('qcml',)
 
 
@@ -78,7 +78,8 @@ class AnalyzingHiC3DeFDR(object):
                                                    self.dist_thresh_max)
         eprint('  computing size factors', skip=not verbose)
         dist = col - row
-        size_factors = ctx.size_factors_cmor(balanced, dist, n_bins or 0)
+        # analysis.py:104-108: conditional norms see the distances
+        size_factors = ctx.size_factors(balanced, dist, norm, n_bins or 0)
         scaled = balanced / size_factors
         design = np.asarray(self.design, dtype=bool)
         mean = np.dot(scaled, design) / np.sum(design, axis=0)
@@ -112,7 +113,13 @@ class AnalyzingHiC3DeFDR(object):
             sl = slice(offsets[i], offsets[i + 1])
             di = disp_idx[disp_idx_offsets[i]:disp_idx_offsets[i + 1]]
             bias = self.load_bias(chrom)
-            sf = self.load_data('size_factors', chrom)[di]
+            sf = self.load_data('size_factors', chrom)
+            # per-replicate (1-D) factors of the non-conditional norms
+            # broadcast over the pixels, as lrt uses them (analysis.py:272-275).
+            # Deviation: the reference indexes them with the pixel mask here
+            # (analysis.py:181) and raises IndexError.
+            if sf.ndim == 2:
+                sf = sf[di]
             f[sl] = bias[row[sl], :] * bias[col[sl], :] * sf
         return raw, f, dist, offsets
 

@@ -16,6 +16,8 @@
 
 #include <cstdint>
 
+#include "h3d_model.h"
+
 namespace h3d {
 
 // (the union state PrepUnion lives in h3d_ctx.h, inside the h3d_ctx)
@@ -174,13 +176,15 @@ __global__ void k_mor_keys(const double* __restrict__ balanced,
        k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = perm[k];
     bool ok = true;
-    double s = 0.0;
+    // gmean(x, pseudocount 1) = exp(nanmean(log(x + 1))) - 1 over the row:
+    // numpy's row reduction (sequential below 8 replicates, pairwise from 8)
+    double lg[kMaxReps];
     for (int r = 0; r < R; ++r) {
       const double v = balanced[i * R + r];
       ok = ok && (v > 0.0);
-      s += log(v + 1);
+      lg[r] = log(v + 1);
     }
-    const double gm = exp(s / R) - 1;
+    const double gm = exp(np_sum<kMaxReps>(lg, R) / R) - 1;
     for (int r = 0; r < R; ++r)
       keys[(int64_t)r * n + k] = ok ? balanced[i * R + r] / gm : INFINITY;
     // valid rows per bin: bins are sorted along k, so a wave spans one or
@@ -275,6 +279,42 @@ __global__ void k_sf_exact(const int32_t* __restrict__ perm,
     const int64_t i = perm[k];
     for (int r = 0; r < R; ++r) sf[i * R + r] = s_per_bin[(int64_t)bin[k] * R + r];
   }
+}
+
+// bin of every pixel in its original position (bin_of_sorted scattered
+// through the distance sort's permutation)
+__global__ void k_scatter_bin(const int32_t* __restrict__ perm,
+                              const int32_t* __restrict__ bin_of_sorted,
+                              int64_t n, int32_t* __restrict__ bin_orig) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x)
+    bin_orig[perm[k]] = bin_of_sorted[k];
+}
+
+// simple_scaling's column sums per (bin, replicate) (scaling.py:64:
+// np.sum(data, axis=0) over the bin's rows in their original order, which
+// numpy accumulates row by row): one lane per (bin, replicate) walks the
+// bin's members (grouped by bin, original order inside) sequentially
+__global__ void k_bin_colsum(const double* __restrict__ balanced,
+                             const int32_t* __restrict__ members,
+                             const int64_t* __restrict__ bin_start, int n_bins,
+                             int R, double* __restrict__ colsum) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_bins * R) return;
+  const int b = t / R, r = t - (t / R) * R;
+  const int64_t e = bin_start[b + 1];
+  double s = 0.0;
+  int64_t k = bin_start[b];
+  // the loads are independent: keep 8 in flight ahead of the dependent adds
+  for (; k + 8 <= e; k += 8) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = balanced[(int64_t)members[k + j] * R + r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; k < e; ++k) s += balanced[(int64_t)members[k] * R + r];
+  colsum[(int64_t)b * R + r] = s;
 }
 
 // exact mode bins: bin of sorted position = its distance rank among distinct

@@ -143,12 +143,25 @@ int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
   return 0;
 }
 
-int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
-                          const int32_t* dist, int64_t n, int R, int n_bins,
-                          double* sf_out) {
-  if (!ctx || (n > 0 && (!balanced || !dist || !sf_out))) return fail(H3D_EARG, "null argument");
+int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
+                     int64_t n, int R, int norm, int n_bins, double* sf_out) {
+  if (!ctx || (n > 0 && !balanced) || !sf_out) return fail(H3D_EARG, "null argument");
   if (R < 1 || R > kMaxReps || n_bins < 0) return fail(H3D_EARG, "R=%d n_bins=%d", R, n_bins);
-  if (n == 0) return 0;
+  if (norm < H3D_NORM_CONDITIONAL_MOR || norm > H3D_NORM_NO_SCALING)
+    return fail(H3D_EARG, "norm %d", norm);
+  const bool conditional =
+      norm == H3D_NORM_CONDITIONAL_MOR || norm == H3D_NORM_CONDITIONAL_SCALING;
+  const bool mor = norm == H3D_NORM_CONDITIONAL_MOR || norm == H3D_NORM_MEDIAN_OF_RATIOS;
+  if (norm == H3D_NORM_NO_SCALING) {  // scaling.py:24: ones(R), no data pass
+    for (int r = 0; r < R; ++r) sf_out[r] = 1.0;
+    return 0;
+  }
+  if (conditional && n > 0 && !dist) return fail(H3D_EARG, "null dist");
+  if (n == 0) {
+    if (!conditional)
+      for (int r = 0; r < R; ++r) sf_out[r] = NAN;  // median / sums of nothing
+    return 0;
+  }
   if (n >= ((int64_t)1 << 31) / R) return fail(H3D_EARG, "n too large");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
@@ -158,84 +171,144 @@ int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
   int32_t* d_idx = (int32_t*)scratch(ctx, "sf_idx", n * 4);
   int32_t* d_perm = (int32_t*)scratch(ctx, "sf_perm", n * 4);
   int32_t* d_bin = (int32_t*)scratch(ctx, "sf_bin", n * 4);
-  double* d_keys = (double*)scratch(ctx, "sf_keys", n * R * 8);
-  double* d_keys_s = (double*)scratch(ctx, "sf_keys_s", n * R * 8);
   double* d_sf = (double*)scratch(ctx, "sf_out", n * R * 8);
-  if (!d_bal || !d_dist || !d_dist_s || !d_idx || !d_perm || !d_bin || !d_keys ||
-      !d_keys_s || !d_sf)
+  if (!d_bal || !d_dist || !d_dist_s || !d_idx || !d_perm || !d_bin || !d_sf)
     return fail(H3D_ENOMEM, "size factor scratch");
   HIP_TRY(hipMemcpyAsync(d_bal, balanced, n * R * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
-  // stable sort by distance (the pinned equal_bin tie order)
   hipLaunchKernelGGL(k_iota, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_idx, n);
   size_t tb = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_dist, d_dist_s, d_idx, d_perm,
-                                             (int)n, 0, 31, s));
-  void* tmp = scratch(ctx, "cub_tmp_sf", tb);
-  if (!tmp) return fail(H3D_ENOMEM, "sort temp");
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_dist, d_dist_s, d_idx, d_perm,
-                                             (int)n, 0, 31, s));
-  int nb = n_bins;
-  if (n_bins > 0) {
-    hipLaunchKernelGGL(k_equal_bin, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, n,
-                       n_bins, d_bin);
+  void* tmp = nullptr;
+  // 1. bins over the (stable) distance order: sorted position k -> bin[k]
+  int nb = 1;
+  if (!conditional) {
+    // one bin holding every pixel, in the original order
+    HIP_TRY(hipMemcpyAsync(d_perm, d_idx, n * 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemsetAsync(d_bin, 0, n * 4, s));
   } else {
-    int32_t* d_head = (int32_t*)scratch(ctx, "sf_head", n * 4);
-    if (!d_head) return fail(H3D_ENOMEM, "heads");
-    hipLaunchKernelGGL(k_dist_heads, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                       d_dist_s, n, d_head);
-    tb = 0;
-    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_head, d_bin, (int)n, s));
-    tmp = scratch(ctx, "cub_tmp_s", tb);
-    if (!tmp) return fail(H3D_ENOMEM, "scan temp");
-    HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, d_bin, (int)n, s));
-    hipLaunchKernelGGL(k_minus_one, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bin, n);
-    int32_t last = 0;
-    HIP_TRY(hipMemcpyAsync(&last, d_bin + n - 1, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    nb = last + 1;
+    HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
+    // stable sort by distance (the pinned equal_bin tie order)
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_dist, d_dist_s, d_idx,
+                                               d_perm, (int)n, 0, 31, s));
+    tmp = scratch(ctx, "cub_tmp_sf", tb);
+    if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_dist, d_dist_s, d_idx, d_perm,
+                                               (int)n, 0, 31, s));
+    if (n_bins > 0) {
+      nb = n_bins;
+      hipLaunchKernelGGL(k_equal_bin, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, n,
+                         n_bins, d_bin);
+    } else {
+      int32_t* d_head = (int32_t*)scratch(ctx, "sf_head", n * 4);
+      if (!d_head) return fail(H3D_ENOMEM, "heads");
+      hipLaunchKernelGGL(k_dist_heads, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         d_dist_s, n, d_head);
+      tb = 0;
+      HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_head, d_bin, (int)n, s));
+      tmp = scratch(ctx, "cub_tmp_s", tb);
+      if (!tmp) return fail(H3D_ENOMEM, "scan temp");
+      HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, d_bin, (int)n, s));
+      hipLaunchKernelGGL(k_minus_one, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bin, n);
+      int32_t last = 0;
+      HIP_TRY(hipMemcpyAsync(&last, d_bin + n - 1, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      nb = last + 1;
+    }
   }
   int64_t* d_bstart = (int64_t*)scratch(ctx, "sf_bstart", (size_t)(nb + 1) * 8);
-  int32_t* d_valid = (int32_t*)scratch(ctx, "sf_valid", (size_t)nb * 4);
   double* d_spb = (double*)scratch(ctx, "sf_spb", (size_t)nb * R * 8);
   double* d_dpb = (double*)scratch(ctx, "sf_dpb", (size_t)nb * 8);
-  int64_t* d_segb = (int64_t*)scratch(ctx, "sf_segb", (size_t)nb * R * 8);
-  int64_t* d_sege = (int64_t*)scratch(ctx, "sf_sege", (size_t)nb * R * 8);
-  if (!d_bstart || !d_valid || !d_spb || !d_dpb || !d_segb || !d_sege)
-    return fail(H3D_ENOMEM, "bins");
+  if (!d_bstart || !d_spb || !d_dpb) return fail(H3D_ENOMEM, "bins");
   hipLaunchKernelGGL(k_bin_bounds, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_bin,
                      n, nb, d_bstart);
-  HIP_TRY(hipMemsetAsync(d_valid, 0, (size_t)nb * 4, s));
-  hipLaunchKernelGGL(k_mor_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bal,
-                     d_perm, n, R, d_bin, d_keys, d_valid);
   std::vector<int64_t> bstart(nb + 1);
   HIP_TRY(hipMemcpyAsync(bstart.data(), d_bstart, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  std::vector<int64_t> segb((size_t)nb * R), sege((size_t)nb * R);
-  for (int r = 0; r < R; ++r)
-    for (int b = 0; b < nb; ++b) {
-      segb[(size_t)r * nb + b] = (int64_t)r * n + bstart[b];
-      sege[(size_t)r * nb + b] = (int64_t)r * n + bstart[b + 1];
-    }
-  HIP_TRY(hipMemcpyAsync(d_segb, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(d_sege, sege.data(), sege.size() * 8, hipMemcpyHostToDevice, s));
-  tb = 0;
-  HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, d_keys, d_keys_s,
-                                                     (int)(n * R), nb * R, d_segb, d_sege,
-                                                     0, 64, s));
-  tmp = scratch(ctx, "cub_tmp_seg", tb);
-  if (!tmp) return fail(H3D_ENOMEM, "segmented sort temp");
-  HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tb, d_keys, d_keys_s,
-                                                     (int)(n * R), nb * R, d_segb, d_sege,
-                                                     0, 64, s));
-  hipLaunchKernelGGL(k_mor_median, dim3((nb * R + 255) / 256), dim3(256), 0, s, d_keys_s,
-                     d_bstart, d_valid, nb, n, R, d_spb);
-  if (n_bins > 0) {
-    hipLaunchKernelGGL(k_bin_dist_sum, dim3(nb), dim3(256), 0, s, d_dist_s,
-                       d_bstart, nb, d_dpb);
-    std::vector<double> dpb(nb), spb((size_t)nb * R);
-    HIP_TRY(hipMemcpyAsync(dpb.data(), d_dpb, nb * 8, hipMemcpyDeviceToHost, s));
+  // 2. per-bin factors s_per_bin (nb, R)
+  std::vector<double> spb((size_t)nb * R);
+  if (mor) {
+    // median_of_ratios (scaling.py:27-47): per replicate the median over the
+    // bin's all-positive rows of data / gmean(row); a segmented sort of the
+    // ratios per (replicate, bin), invalid rows keyed +inf past the valid ones
+    int32_t* d_valid = (int32_t*)scratch(ctx, "sf_valid", (size_t)nb * 4);
+    double* d_keys = (double*)scratch(ctx, "sf_keys", n * R * 8);
+    double* d_keys_s = (double*)scratch(ctx, "sf_keys_s", n * R * 8);
+    int64_t* d_segb = (int64_t*)scratch(ctx, "sf_segb", (size_t)nb * R * 8);
+    int64_t* d_sege = (int64_t*)scratch(ctx, "sf_sege", (size_t)nb * R * 8);
+    if (!d_valid || !d_keys || !d_keys_s || !d_segb || !d_sege)
+      return fail(H3D_ENOMEM, "median scratch");
+    HIP_TRY(hipMemsetAsync(d_valid, 0, (size_t)nb * 4, s));
+    hipLaunchKernelGGL(k_mor_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bal,
+                       d_perm, n, R, d_bin, d_keys, d_valid);
+    std::vector<int64_t> segb((size_t)nb * R), sege((size_t)nb * R);
+    for (int r = 0; r < R; ++r)
+      for (int b = 0; b < nb; ++b) {
+        segb[(size_t)r * nb + b] = (int64_t)r * n + bstart[b];
+        sege[(size_t)r * nb + b] = (int64_t)r * n + bstart[b + 1];
+      }
+    HIP_TRY(hipMemcpyAsync(d_segb, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_sege, sege.data(), sege.size() * 8, hipMemcpyHostToDevice, s));
+    tb = 0;
+    HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, d_keys, d_keys_s,
+                                                       (int)(n * R), nb * R, d_segb,
+                                                       d_sege, 0, 64, s));
+    tmp = scratch(ctx, "cub_tmp_seg", tb);
+    if (!tmp) return fail(H3D_ENOMEM, "segmented sort temp");
+    HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tb, d_keys, d_keys_s,
+                                                       (int)(n * R), nb * R, d_segb,
+                                                       d_sege, 0, 64, s));
+    hipLaunchKernelGGL(k_mor_median, dim3((nb * R + 255) / 256), dim3(256), 0, s,
+                       d_keys_s, d_bstart, d_valid, nb, n, R, d_spb);
     HIP_TRY(hipMemcpyAsync(spb.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else {
+    // simple_scaling (scaling.py:50-65): column sums over the bin's rows in
+    // their original order (members grouped by bin: a stable sort of the
+    // original-order bin labels), then s / gmean(s, pseudocount 1)
+    int32_t* members = d_idx;
+    if (conditional) {
+      int32_t* d_bin_orig = (int32_t*)scratch(ctx, "sf_bin_orig", n * 4);
+      int32_t* d_bin_orig_s = (int32_t*)scratch(ctx, "sf_bin_orig_s", n * 4);
+      int32_t* d_iota = (int32_t*)scratch(ctx, "sf_iota2", n * 4);
+      members = (int32_t*)scratch(ctx, "sf_members", n * 4);
+      if (!d_bin_orig || !d_bin_orig_s || !d_iota || !members)
+        return fail(H3D_ENOMEM, "member scratch");
+      hipLaunchKernelGGL(k_scatter_bin, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         d_perm, d_bin, n, d_bin_orig);
+      hipLaunchKernelGGL(k_iota, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_iota, n);
+      int end_bit = 1;
+      while (end_bit < 31 && (1 << end_bit) <= nb) ++end_bit;
+      tb = 0;
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_bin_orig, d_bin_orig_s,
+                                                 d_iota, members, (int)n, 0, end_bit, s));
+      tmp = scratch(ctx, "cub_tmp_sf", tb);
+      if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_bin_orig, d_bin_orig_s, d_iota,
+                                                 members, (int)n, 0, end_bit, s));
+    }
+    hipLaunchKernelGGL(k_bin_colsum, dim3((nb * R + 255) / 256), dim3(256), 0, s, d_bal,
+                       members, d_bstart, nb, R, d_spb);
+    std::vector<double> colsum((size_t)nb * R);
+    HIP_TRY(hipMemcpyAsync(colsum.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost,
+                           s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int b = 0; b < nb; ++b) {
+      const double* cs = &colsum[(size_t)b * R];
+      double lg[kMaxReps];
+      for (int r = 0; r < R; ++r) lg[r] = std::log(cs[r] + 1);
+      const double gm = std::exp(np_sum<kMaxReps>(lg, R) / R) - 1;
+      for (int r = 0; r < R; ++r) spb[(size_t)b * R + r] = cs[r] / gm;
+    }
+  }
+  if (!conditional) {
+    std::memcpy(sf_out, spb.data(), R * 8);
+    return 0;
+  }
+  // 3. per-pixel factors (scaling.py:88-105)
+  if (n_bins > 0) {
+    hipLaunchKernelGGL(k_bin_dist_sum, dim3(nb), dim3(256), 0, s, d_dist_s, d_bstart, nb,
+                       d_dpb);
+    std::vector<double> dpb(nb);
+    HIP_TRY(hipMemcpyAsync(dpb.data(), d_dpb, nb * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // np.unique(bins): only non-empty bins take part in the interpolation
     std::vector<double> xp, yp;
@@ -254,12 +327,20 @@ int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
     hipLaunchKernelGGL(k_sf_interp, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_dist, n,
                        R, d_xp, d_yp, m, d_sf);
   } else {
+    HIP_TRY(hipMemcpyAsync(d_spb, spb.data(), (size_t)nb * R * 8, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_sf_exact, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_perm,
                        d_bin, n, R, d_spb, d_sf);
   }
   HIP_TRY(hipMemcpyAsync(sf_out, d_sf, n * R * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return 0;
+}
+
+int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
+                          const int32_t* dist, int64_t n, int R, int n_bins,
+                          double* sf_out) {
+  return h3d_size_factors(ctx, balanced, dist, n, R, H3D_NORM_CONDITIONAL_MOR, n_bins,
+                          sf_out);
 }
 
 }  // extern "C"

@@ -7,6 +7,8 @@
  *   h3d_union_*            <- util/matrices.py:92-129 sparse_union (+ the raw /
  *                              balanced gathers, analysis/analysis.py:91-101)
  *   h3d_size_factors_cmor  <- util/scaling.py:108-127 conditional_mor
+ *   h3d_size_factors       <- util/scaling.py:10-149 (every norm prepare_data
+ *                              dispatches, analysis/analysis.py:104-108)
  *   h3d_disp_per_dist      <- analysis/analysis.py:185-206 (estimator per
  *                              distance/condition; util/dispersion.py:10-80
  *                              qcml/cml, util/scaled_nb.py:71-275)
@@ -52,6 +54,13 @@ extern "C" {
 #define H3D_EST_QCML 0
 #define H3D_EST_CML 1
 #define H3D_EST_MME 2
+
+/* size-factor methods (util/scaling.py) */
+#define H3D_NORM_CONDITIONAL_MOR 0     /* :108-127, (n, R)                */
+#define H3D_NORM_CONDITIONAL_SCALING 1 /* :130-149, (n, R)                */
+#define H3D_NORM_MEDIAN_OF_RATIOS 2    /* :27-47, (R,)                    */
+#define H3D_NORM_SIMPLE_SCALING 3      /* :50-65, (R,)                    */
+#define H3D_NORM_NO_SCALING 4          /* :10-24, (R,)                    */
 
 /* per-segment / per-pixel status bits (also in *flags outputs) */
 #define H3D_FLAG_NOROOT 1   /* all-zero counts: no MLE (ref ValueError)      */
@@ -99,6 +108,14 @@ int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
 int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
                           const int32_t* dist, int64_t n, int R, int n_bins,
                           double* sf_out);
+
+/* Size factors of any norm (scaling.py): the conditional methods condition
+ * on distance (n_bins equal-number bins, or exact distances when n_bins ==
+ * 0; scaling.py:68-105) and write sf (n, R); the global ones write one
+ * factor per replicate, sf (R). balanced (n, R), dist (n; unused by the
+ * global methods, may be NULL). */
+int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
+                     int64_t n, int R, int norm, int n_bins, double* sf_out);
 
 /* ---- estimate_disp ----------------------------------------------------- */
 

@@ -58,11 +58,27 @@ def binary(lib, name, a, x):
     return out
 
 
+def igam_err(got, ref, a, x):
+    """Largest error of an incomplete-gamma value in units of its tolerance
+    1e-12 + 2 ulp x |a ln x| + |x| + |lgamma a|: the regularised prefactor
+    exp(a ln x - x - lgamma a) turns the rounding of that exponent (~1e4 at a
+    = 2e3) into relative error, for scipy's evaluation as much as for this
+    one, so two correct libms (glibc on the host, OCML on gfx950) differ by
+    that much (measured on gfx950: 1.8e-12 at a ~ 2e3)."""
+    got, ref = np.asarray(got), np.asarray(ref)
+    with np.errstate(all='ignore'):
+        scale = np.abs(a * np.log(x)) + np.abs(x) + np.abs(sc.gammaln(a))
+        tol = 1e-12 + 2 * 2.2e-16 * np.where(np.isfinite(scale), scale, 0)
+        err = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)
+    err[(got == ref) | (np.isnan(got) & np.isnan(ref))] = 0
+    return float(np.max(err / tol))
+
+
 def test_special_vs_reference_goldens(lib):
     g = golden('unit_special.npz')
     a, x, p = g['a'], g['x'], g['p']
-    assert rel_err(binary(lib, 'igam', a, x), g['gammainc']) < 1e-12
-    assert rel_err(binary(lib, 'igamc', a, x), g['gammaincc']) < 1e-12
+    assert igam_err(binary(lib, 'igam', a, x), g['gammainc'], a, x) < 1
+    assert igam_err(binary(lib, 'igamc', a, x), g['gammaincc'], a, x) < 1
     assert rel_err(binary(lib, 'igami', a, p), g['gammaincinv']) < 1e-11
     assert rel_err(binary(lib, 'igamci', a, p), g['gammainccinv']) < 1e-11
     assert rel_err(unary(lib, 'ndtr', g['z']), g['ndtr']) < 1e-13
@@ -79,8 +95,8 @@ def test_special_dense_grids(lib):
     # shapes/arguments met in q2qnbinom: a = mu/(1+alpha mu) in [1e-3, 2e3]
     a = np.concatenate([10 ** rng.uniform(-3, 3.3, 20000)])
     x = a * np.exp(rng.normal(0, 0.5, a.size))
-    assert rel_err(binary(lib, 'igam', a, x), sc.gammainc(a, x)) < 1e-12
-    assert rel_err(binary(lib, 'igamc', a, x), sc.gammaincc(a, x)) < 1e-12
+    assert igam_err(binary(lib, 'igam', a, x), sc.gammainc(a, x), a, x) < 1
+    assert igam_err(binary(lib, 'igamc', a, x), sc.gammaincc(a, x), a, x) < 1
     q = np.clip(rng.uniform(0, 1, a.size) ** 4, 1e-300, 1 - 1e-16)
     assert rel_err(binary(lib, 'igami', a, q), sc.gammaincinv(a, q)) < 1e-11
     assert rel_err(binary(lib, 'igamci', a, q), sc.gammainccinv(a, q)) < 1e-11
