@@ -8,9 +8,17 @@ disp pixels to HBM. One step = estimate_disp (qcml per distance x condition,
 lowess smoothing table) + lrt (fused per-pixel GLM fits + LRT) on the
 resident inputs, outputs left in HBM.
 
-N > 1 (torchrun, one rank per GPU over RCCL): weak scaling — every rank owns
+N > 1 (torchrun, one rank per GPU over RCCL): weak scaling -- every rank owns
 its own chromosome; the genome-wide per-distance pooling of estimate_disp is
 kept by an all-reduce of the per-segment NLL sums each data pass.
+
+The CPU baseline (rank 0, N = 1) runs FIRST, before anything touches the GPU
+(its worker pool forks): the CPU restatement (oracle/, numpy/scipy) with the
+reference's parallel structure on min(os.cpu_count(), 16) processes, median
+of 4 runs, on a bounded sample; two rows: fallback-fixed (brentq only on the
+failed pixel) and faithful (the reference's O(fail * N) brentq fallback,
+scaled_nb.py:162-181, LRT on one process per chromosome as
+analysis.py:247-257).
 
 Prints ONE JSON line on rank 0.
 """
@@ -18,6 +26,7 @@ import argparse
 import json
 import os
 import shutil
+import statistics
 import sys
 import tempfile
 import time
@@ -30,37 +39,198 @@ import numpy as np  # noqa: E402
 METRIC = ("pixels/sec through estimate_disp+lrt, 4 reps @10kb; "
           "max-|Δq| vs reference")
 
+PMC_SUMMARY = os.path.join(REPO, 'profiles', 'pmc_default.json')
+FP64_PEAK_TFLOPS = 78.6   # MI355X vector FP64, dense (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+CPU_RUNS = 4
 
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                           'profiles', 'pmc_traffic_default.json')
 
+# ---------------------------------------------------------------------------
+# committed PMC summary (tools/pmc_passes.sh over the default command)
+# ---------------------------------------------------------------------------
 
-def pmc_traffic(kernel, bins, dmax):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (tools/pmc_passes.sh over this same default command: FETCH_SIZE x2
-    gfx950 correction + WRITE_SIZE, each its own rocprofv3 pass).  Counters
-    cannot be read inside the timed run, so the figure comes from that
-    profile; None unless the workload is the one it was measured on."""
+def pmc_kernel(kernel, bins, dmax):
+    """Per-launch counters of `kernel` (name prefix) from the committed PMC
+    summary of this same default command: HBM bytes (FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE), FP64 flops issued ((ADD + MUL + TRANS + 2 FMA)
+    x 64 lanes), lane utilisation. Counters cannot be read inside the timed
+    run; None unless the workload is the one they were measured on."""
     try:
         d = json.load(open(PMC_SUMMARY))
     except (OSError, ValueError):
         return None
     if d.get('bins') != bins or d.get('dmax') != dmax:
         return None
-    rd = wr = 0.0
-    n = 0
+    acc, n = {}, 0
     for key, e in d['kernels'].items():
-        if kernel in key.split('[')[0]:
-            rd += e.get('hbm_read_bytes_corrected', 0.0)
-            wr += e.get('hbm_write_bytes', 0.0)
-            n += e['dispatches']
-    return (rd + wr) / n if n else None
+        if not key.split('[')[0].split('(')[0].strip().endswith(kernel):
+            continue
+        n += e['dispatches']
+        for c in ('hbm_read_bytes_corrected', 'hbm_write_bytes',
+                  'SQ_INSTS_VALU_ADD_F64', 'SQ_INSTS_VALU_MUL_F64',
+                  'SQ_INSTS_VALU_FMA_F64', 'SQ_INSTS_VALU_TRANS_F64',
+                  'SQ_THREAD_CYCLES_VALU', 'SQ_ACTIVE_INST_VALU'):
+            acc[c] = acc.get(c, 0.0) + e.get(c, 0.0)
+    if not n:
+        return None
+    flops = 64.0 * (acc['SQ_INSTS_VALU_ADD_F64'] + acc['SQ_INSTS_VALU_MUL_F64']
+                    + acc['SQ_INSTS_VALU_TRANS_F64']
+                    + 2.0 * acc['SQ_INSTS_VALU_FMA_F64'])
+    lu = acc['SQ_THREAD_CYCLES_VALU'] / (64.0 * acc['SQ_ACTIVE_INST_VALU']) \
+        if acc['SQ_ACTIVE_INST_VALU'] else None
+    return {'hbm_bytes': (acc['hbm_read_bytes_corrected'] +
+                          acc['hbm_write_bytes']) / n,
+            'f64_flops': flops / n, 'lane_util': lu, 'dispatches': n}
 
 
 def bytes_per_lrt_pixel(R, C):
     # raw int32 4R + f 8R + dist 4 in; p, llr, mu0 24 + mu1 8C + disp 8C out
     return 12 * R + 16 * C + 28
 
+
+def fp64_roof(pmc, avg_s):
+    if not pmc or not avg_s:
+        return None
+    ach = pmc['f64_flops'] / avg_s / 1e12
+    out = {'achieved': ach, 'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+           'frac': ach / FP64_PEAK_TFLOPS,
+           'flops_per_launch': pmc['f64_flops'],
+           'lane_util': pmc['lane_util']}
+    if pmc['lane_util'] is not None:
+        out['useful_frac'] = out['frac'] * pmc['lane_util']
+    return out
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (runs before the GPU is touched)
+# ---------------------------------------------------------------------------
+
+def _qcml_task(args):
+    import oracle
+    data, f, faithful = args
+    return oracle.qcml(data, f=f, faithful=faithful) if data.size else np.nan
+
+
+def _lrt_task(args):
+    import oracle
+    raw, f, dw, design, faithful = args
+    return oracle.lrt(raw, f, dw, design, faithful=faithful)[0]
+
+
+def cpu_pipeline(pool, workers, raw, f, dist, design, D, faithful):
+    """estimate_disp + lrt on the CPU with the reference's parallel structure:
+    qcml per (distance, condition) over the pool (analysis.py:193-200), the
+    lowess fit per condition, then the LRT -- faithful: one call over the
+    chromosome (one process per chromosome, analysis.py:247-257);
+    fallback-fixed: pixel blocks over the pool. Returns p."""
+    import oracle
+    C = design.shape[1]
+    order = np.argsort(dist, kind='stable')
+    bounds = np.searchsorted(dist[order], np.arange(D + 1))
+    tasks = []
+    for c in range(C):
+        cols = design[:, c]
+        for d in range(D):
+            sel = order[bounds[d]:bounds[d + 1]]
+            tasks.append((raw[sel][:, cols], f[sel][:, cols], faithful))
+    dpd = np.array(pool.map(_qcml_task, tasks, chunksize=4)).reshape(C, D).T
+    disp = np.zeros((len(raw), C))
+    for c in range(C):
+        fin = np.isfinite(dpd[:, c])
+        x, y = np.arange(D)[fin], dpd[fin, c]
+        disp[:, c] = oracle.weighted_lowess_fit(x, y, left_boundary=y[0])(dist)
+    dw = np.dot(disp, design.T)
+    if faithful:
+        return _lrt_task((raw, f, dw, design, True))
+    blocks = np.array_split(np.arange(len(raw)), workers * 4)
+    return np.concatenate(pool.map(
+        _lrt_task, [(raw[b], f[b], dw[b], design, False) for b in blocks]))
+
+
+def cpu_baseline_run(bins, dmax, seed=123):
+    import multiprocessing
+    import oracle
+    from hic3defdr_amd import synthetic
+    tmp = tempfile.mkdtemp(prefix='h3dbench_cpu_')
+    try:
+        kw = synthetic.write_dataset(tmp, {'chrS': bins}, dist_thresh_max=dmax,
+                                     seed=seed)
+        design = kw['design']
+        npz = [p.replace('<chrom>', 'chrS') for p in kw['raw_npz_patterns']]
+        bfs = [p.replace('<chrom>', 'chrS') for p in kw['bias_patterns']]
+        prep = oracle.prepare_chrom(npz, bfs, design, dist_thresh_max=dmax)
+        bias = oracle.load_bias(bfs)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    di = prep['disp_idx']
+    row, col = prep['row'][di], prep['col'][di]
+    raw = prep['raw'][di]
+    f = bias[row] * bias[col] * prep['size_factors'][di]
+    dist = col - row
+    n = len(raw)
+    ncpu = os.cpu_count() or 1
+    workers = max(1, min(ncpu, 16))   # the GPU box's CPU share per GPU
+    rows, p_out = {}, {}
+    ctx = multiprocessing.get_context('fork')
+    with ctx.Pool(workers) as pool:
+        for faithful in (False, True):
+            times = []
+            for _ in range(CPU_RUNS):
+                t0 = time.perf_counter()
+                p = cpu_pipeline(pool, workers, raw, f, dist, design, dmax + 1,
+                                 faithful)
+                times.append(time.perf_counter() - t0)
+            med = statistics.median(times)
+            rows[faithful] = {'value': n / med, 'median_s': med,
+                              'runs_s': times}
+            p_out[faithful] = p
+    sample = ('1 synthetic chrom of %d bins (seed %d), dmax %d, 4 reps 2+2: '
+              '%d disp pixels; median of %d runs' % (bins, seed, dmax, n,
+                                                     CPU_RUNS))
+    base = {'value': rows[False]['value'], 'unit': 'pixels/s',
+            'cores': workers, 'cpu_count': ncpu, 'kind': 'port',
+            'variant': 'fallback-fixed (brentq on the failed pixel only; '
+                       'LRT over pixel blocks on the pool)',
+            'median_s': rows[False]['median_s'],
+            'runs_s': rows[False]['runs_s'], 'sample': sample,
+            'faithful': {'value': rows[True]['value'], 'unit': 'pixels/s',
+                         'cores': workers,
+                         'variant': 'faithful O(fail*N) brentq '
+                                    '(scaled_nb.py:162-181); qcml on the '
+                                    'pool, LRT one process per chromosome',
+                         'median_s': rows[True]['median_s'],
+                         'runs_s': rows[True]['runs_s']}}
+    return base, {'raw': raw, 'f': f, 'dist': dist, 'design': design,
+                  'p_fixed': p_out[False], 'p_faithful': p_out[True]}
+
+
+def sample_parity(ctx, sample, dmax):
+    """The GPU on the CPU baseline's sample: p / q agreement and calls."""
+    import oracle
+    from hic3defdr_amd import _native
+    design = sample['design']
+    cond = design.argmax(axis=1)
+    C = design.shape[1]
+    out = ctx.disp_per_dist(sample['raw'], sample['f'], sample['dist'], cond,
+                            C, dmax + 1)
+    tab = _native.disp_tables(out)
+    p, _, _, _, _ = ctx.lrt(sample['raw'], sample['f'], sample['dist'], tab,
+                            cond)
+    qg = _native.bh(p)
+    res = {'sample_pixels': int(len(p))}
+    for name, rp in (('fixed', sample['p_fixed']),
+                     ('faithful', sample['p_faithful'])):
+        qo = oracle.adjust_pvalues(rp)
+        with np.errstate(all='ignore'):
+            res['max_rel_dp_vs_cpu_%s' % name] = float(
+                np.nanmax(np.abs(p - rp) / np.maximum(rp, 1e-300)))
+            res['max_abs_dq_vs_cpu_%s' % name] = float(np.nanmax(np.abs(qg - qo)))
+        res['identical_calls_q<0.05_%s' % name] = bool(
+            np.array_equal(qg < 0.05, qo < 0.05))
+    return res
+
+
+# ---------------------------------------------------------------------------
 
 def make_workload(tmp, name, bins, dmax, seed):
     import pandas as pd
@@ -75,54 +245,30 @@ def make_workload(tmp, name, bins, dmax, seed):
     return h, kw
 
 
-def cpu_baseline(ctx, bins, dmax, seed=123):
-    """The oracle (numpy/scipy restatement, fallback-fixed brentq) timed on a
-    bounded sample of the same workload, 1 core; plus the GPU on the same
-    sample for a parity figure."""
-    import oracle
-    from hic3defdr_amd import synthetic, _native
-    tmp = tempfile.mkdtemp(prefix='h3dbench_cpu_')
-    try:
-        kw = synthetic.write_dataset(tmp, {'chrS': bins}, dist_thresh_max=dmax,
-                                     seed=seed)
-        design = kw['design']
-        npz = [p.replace('<chrom>', 'chrS') for p in kw['raw_npz_patterns']]
-        bfs = [p.replace('<chrom>', 'chrS') for p in kw['bias_patterns']]
-        prep = oracle.prepare_chrom(npz, bfs, design, dist_thresh_max=dmax)
-        bias = oracle.load_bias(bfs)
-        di = prep['disp_idx']
-        row, col = prep['row'][di], prep['col'][di]
-        raw = prep['raw'][di]
-        f = bias[row] * bias[col] * prep['size_factors'][di]
-        t0 = time.time()
-        disp, dpd, _ = oracle.estimate_disp([prep], [bias], design,
-                                            dist_thresh_max=dmax)
-        rp, _, _, _ = oracle.lrt(raw, f, np.dot(disp, design.T), design)
-        dt = time.time() - t0
-        n = len(raw)
-        # GPU on the same sample
-        cond = design.argmax(axis=1)
-        C = design.shape[1]
-        out = ctx.disp_per_dist(raw, f, col - row, cond, C, dmax + 1)
-        tab = np.stack([_native.disp_table(out[:, c]) for c in range(C)], 1)
-        p, _, _, _, _ = ctx.lrt(raw, f, col - row, tab, cond)
-        qg = _native.bh(p)
-        qo = oracle.adjust_pvalues(rp)
-        with np.errstate(all='ignore'):
-            dp = np.nanmax(np.abs(p - rp) / np.maximum(rp, 1e-300))
-            dq = np.nanmax(np.abs(qg - qo))
-        return {'value': n / dt, 'unit': 'pixels/s', 'cores': 1,
-                'kind': 'port',
-                'sample': 'oracle estimate_disp+lrt (numpy/scipy, brentq '
-                          'fallback per failed pixel) on 1 synthetic chrom '
-                          'of %d bins, dmax %d, 4 reps: %d disp pixels in '
-                          '%.1f s' % (bins, dmax, n, dt)}, \
-            {'sample_pixels': n, 'max_rel_dp_vs_oracle': float(dp),
-             'max_abs_dq_vs_oracle': float(dq),
-             'identical_calls_q<0.05': bool(np.array_equal(qg < 0.05,
-                                                             qo < 0.05))}
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+def e2e_wall(h, tmp):
+    """The product's whole run_to_qvalues on the same workload files (host
+    I/O included), per stage."""
+    from hic3defdr_amd import HiC3DeFDR
+    out = os.path.join(tmp, 'out_e2e')
+    os.makedirs(out, exist_ok=True)
+    h2 = HiC3DeFDR(raw_npz_patterns=h.raw_npz_patterns,
+                   bias_patterns=h.bias_patterns, chroms=h.chroms,
+                   design=h.design, outdir=out,
+                   dist_thresh_max=h.dist_thresh_max)
+    t = [time.perf_counter()]
+    h2.prepare_data(verbose=False)
+    t.append(time.perf_counter())
+    h2.estimate_disp()
+    t.append(time.perf_counter())
+    h2.lrt(verbose=False)
+    t.append(time.perf_counter())
+    h2.bh()
+    t.append(time.perf_counter())
+    return {'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
+            'estimate_disp_s': t[2] - t[1], 'lrt_s': t[3] - t[2],
+            'bh_s': t[4] - t[3],
+            'note': 'HiC3DeFDR.run_to_qvalues stages on the bench workload, '
+                    'NPZ parse and .npy outdir writes included'}
 
 
 def main():
@@ -134,11 +280,15 @@ def main():
     ap.add_argument('--dmax', type=int, default=250)
     ap.add_argument('--cpu-bins', type=int, default=1000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_run(args.cpu_bins, args.dmax)   # before the GPU
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -210,7 +360,7 @@ def main():
         u_ms, u_n, _ = ctx.profile_read('disp_update')
         n_ms, n_n, n_bytes = ctx.profile_read('disp_nll')
         p_ms, p_n, _ = ctx.profile_read('disp_prep')
-        b_ms, _, _ = ctx.profile_read('disp_work')
+        b_ms, b_n, _ = ctx.profile_read('disp_work')
         b_lrt, _, _ = ctx.profile_read('lrt')
         tot_px = n
         if dist:
@@ -222,12 +372,41 @@ def main():
             tot_px = int(t.item())
         value = tot_px * args.steps / elapsed
         if rank == 0:
-            peak = 8000.0
             w_avg_s = (w_ms / max(w_n, 1)) / 1e3
-            w_ach = (w_bytes / max(w_n, 1)) / w_avg_s / 1e9 if w_avg_s else 0.0
+            w_bpl = w_bytes / max(w_n, 1)
+            w_ach = w_bpl / w_avg_s / 1e9 if w_avg_s else 0.0
             l_avg_s = (l_ms / max(l_n, 1)) / 1e3
             l_ach = (n * bytes_per_lrt_pixel(R, C)) / l_avg_s / 1e9 \
                 if l_avg_s else 0.0
+            n_avg_s = (n_ms / max(n_n, 1)) / 1e3
+            eq_pmc = pmc_kernel('k_disp_work<4, 4, 0, false>', args.bins, args.dmax)
+            nll_pmc = pmc_kernel('k_brent<4>', args.bins, args.dmax)
+            lrt_pmc = pmc_kernel('k_lrt<4, 2>', args.bins, args.dmax)
+            eq_fp64 = fp64_roof(eq_pmc, w_avg_s)
+            roof = {
+                'bound': 'fp64', 'kernel': 'k_disp_work<4,4,kEqualize,false> (equalize pass)',
+                'achieved': eq_fp64['achieved'] if eq_fp64 else None,
+                'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                'frac': eq_fp64['frac'] if eq_fp64 else None,
+                'useful_frac': eq_fp64.get('useful_frac') if eq_fp64 else None,
+                'lane_util': eq_pmc['lane_util'] if eq_pmc else None,
+                'flops_per_launch': eq_pmc['f64_flops'] if eq_pmc else None,
+                'flops_source': 'FP64 flops issued per launch, PMC '
+                                '(ADD+MUL+TRANS+2*FMA)_F64 x 64 lanes, '
+                                'profiles/pmc_default.json; useful_frac = '
+                                'frac x lane_util',
+                'traffic': eq_pmc['hbm_bytes'] if eq_pmc else None,
+                'traffic_source': 'PMC HBM bytes per launch (FETCH_SIZE x2 '
+                                  '+ WRITE_SIZE), profiles/pmc_default.json',
+                'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
+                'hbm': {'achieved': w_ach, 'peak': HBM_PEAK_GBS,
+                        'unit': 'GB/s', 'frac': w_ach / HBM_PEAK_GBS,
+                        'bytes_per_launch': w_bpl,
+                        'note': 'algorithmic: 20 B per equalize pixel-'
+                                'replicate (raw 4 + f 8 in, pseudodata 8 '
+                                'out)'},
+                'note': 'FP64-VALU bound (SURVEY.md finding 3): q2qnbinom '
+                        'incomplete-gamma series / continued fractions'}
             out = {
                 'metric': METRIC, 'value': value, 'unit': 'pixels/s',
                 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -242,51 +421,41 @@ def main():
                                 '(qcml) + lrt on HBM-resident inputs'
                                 % (args.bins, args.dmax),
                     'disp_pixels_per_gpu': n, 'disp_pixels_total': tot_px,
-                    'parallelism': 'dp%d (chromosome shards, per-pass '
-                                   'NLL all-reduce)' % world},
-                'roofline': {
-                    'bound': 'hbm', 'kernel': 'k_disp_work',
-                    'achieved': w_ach, 'peak': peak, 'unit': 'GB/s',
-                    'frac': w_ach / peak,
-                    # equalize instantiation <M=4, W=4, kEqualize>
-                    'traffic': pmc_traffic('k_disp_work<4, 4, 0>', args.bins,
-                                           args.dmax),
-                    'traffic_source': 'profiles/pmc_traffic_default.json '
-                                      '(HBM bytes per launch)',
-                    'bytes_per_launch': w_bytes / max(w_n, 1),
-                    'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
-                    'note': 'FP64-VALU/transcendental bound (SURVEY.md '
-                            'finding 3); bytes = 20 B per equalize '
-                            'pixel-replicate (raw 4 + f 8 in, pseudodata 8 '
-                            'out)'},
+                    'parallelism': 'dp%d (chromosome shards; %s)' % (
+                        world, 'in-kernel Brent searches' if world == 1 else
+                        'per-pass NLL all-reduce over RCCL')},
+                'roofline': roof,
+                'kernel_rooflines': {
+                    'nll_k_brent': {
+                        'fp64': fp64_roof(nll_pmc, n_avg_s),
+                        'hbm_traffic_per_launch': nll_pmc['hbm_bytes']
+                        if nll_pmc else None,
+                        'algorithmic_bytes_per_launch': n_bytes / max(n_n, 1),
+                        'avg_launch_us': n_avg_s * 1e6},
+                    'lrt': {'fp64': fp64_roof(lrt_pmc, l_avg_s),
+                            'hbm': {'achieved': l_ach, 'peak': HBM_PEAK_GBS,
+                                    'unit': 'GB/s',
+                                    'frac': l_ach / HBM_PEAK_GBS,
+                                    'bytes_per_pixel':
+                                        bytes_per_lrt_pixel(R, C)},
+                            'hbm_traffic_per_launch': lrt_pmc['hbm_bytes']
+                            if lrt_pmc else None,
+                            'avg_launch_us': l_avg_s * 1e6}},
                 'kernels_ms_per_step': {
                     'note': 'one extra untimed step, every kernel timed',
-                    'disp_work': b_ms,
-                    'disp_reduce': r_ms,
-                    'disp_update': u_ms,
-                    'disp_nll': n_ms,
-                    'disp_prep': p_ms,
-                    'lrt': b_lrt},
+                    'disp_work': b_ms, 'disp_reduce': r_ms,
+                    'disp_update': u_ms, 'disp_nll': n_ms,
+                    'disp_prep': p_ms, 'lrt': b_lrt},
                 'work_per_step': {
                     'equalize_pixel_reps': w_bytes / 20.0 / args.steps,
                     'nll_pixel_reps': n_bytes / 8.0,
-                    'disp_launches': w_n / args.steps},
-                'nll_roofline': {
-                    'achieved': n_bytes / (n_ms / 1e3) / 1e9 if n_ms else 0.0,
-                    'peak': peak, 'unit': 'GB/s',
-                    'frac': n_bytes / (n_ms / 1e3) / 1e9 / peak if n_ms
-                    else 0.0,
-                    'bytes_per_pixel_rep': 8,
-                    'avg_launch_us': n_ms / max(n_n, 1) * 1e3},
-                'lrt_roofline': {'achieved': l_ach, 'peak': peak,
-                                 'unit': 'GB/s', 'frac': l_ach / peak,
-                                 'bytes_per_pixel': bytes_per_lrt_pixel(R, C),
-                                 'avg_launch_us': l_avg_s * 1e6},
+                    'disp_launches': b_n, 'equalize_launches': w_n / args.steps},
             }
-            if world == 1 and not args.no_cpu_baseline:
-                cb, par = cpu_baseline(ctx, args.cpu_bins, args.dmax)
-                out['cpu_baseline'] = cb
-                out['parity_sample'] = par
+            if cpu is not None:
+                out['cpu_baseline'] = cpu[0]
+                out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
+            if world == 1 and not args.no_e2e:
+                out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
             print(json.dumps(out), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

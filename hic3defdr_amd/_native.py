@@ -58,6 +58,16 @@ def load_library(path=None):
             raise H3DError('libh3d.so not found at %s: run '
                            '`python -c "import __graft_entry__ as g; g.build()"`'
                            % p)
+        # One HIP runtime per process: torch (when installed) ships its own
+        # libamdhip64.so.7 under the same SONAME as the /opt/rocm one libh3d
+        # links, and whichever loads first serves both. Loading torch's first
+        # keeps torch.cuda working next to libh3d (the other order leaves
+        # torch without devices) and lets torch tensors / streams be handed
+        # to the *_dev entry points.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(p)
         sig = {
             'h3d_version': (_I, []),

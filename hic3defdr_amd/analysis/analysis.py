@@ -15,15 +15,19 @@ work runs on the GPU through libh3d.so:
                    the cluster JSON / TSV text)
 
 ``n_threads`` is accepted for signature compatibility: the reference's
-process pools (util/parallelization.py) are replaced by the GPU; multi-GPU
-sharding is hic3defdr_amd.parallel.
+process pools (util/parallelization.py) are replaced by the GPU. Under
+torchrun (a torch.distributed process group is initialised) every stage
+shards itself over the ranks (hic3defdr_amd.parallel): each rank owns the
+chromosomes LPT assigns it for prepare_data and lrt, estimate_disp pools
+the distances genome-wide through a per-pass all-reduce of the NLL sums,
+and BH gathers the p-values on rank 0 and scatters the q-values back.
 """
 import os
 
 import numpy as np
 import scipy.sparse as sparse
 
-from hic3defdr_amd import _native
+from hic3defdr_amd import _native, parallel
 from hic3defdr_amd.analysis.core import DispFn
 from hic3defdr_amd.util.classification import classify_clusters
 from hic3defdr_amd.util.cluster_table import ClusterTable
@@ -45,7 +49,16 @@ def _canonical_csr(fname):
 class AnalyzingHiC3DeFDR(object):
 
     def _ctx(self):
-        return _native.context()
+        return _native.context(parallel.device_for_rank())
+
+    def _shards(self):
+        """This rank's chromosomes (all of them without a process group);
+        chromosome sizes read once per object."""
+        sizes = self.__dict__.get('_chrom_sizes')
+        if sizes is None:
+            sizes = parallel.chrom_sizes(self.bias_patterns, self.chroms)
+            self.__dict__['_chrom_sizes'] = sizes
+        return parallel.Shards(self.chroms, sizes)
 
     def _cond_of_rep(self):
         d = np.asarray(self.design, dtype=bool)
@@ -61,9 +74,11 @@ class AnalyzingHiC3DeFDR(object):
         if n_bins == -1:
             n_bins = int(self.dist_thresh_max / 5)
         if chrom is None:
-            for c in self.chroms:
+            sh = self._shards()
+            for c in sh.mine:
                 self.prepare_data(chrom=c, norm=norm, n_bins=n_bins,
                                   verbose=verbose)
+            sh.barrier()
             return
         if norm not in NATIVE_NORMS:
             raise NotImplementedError(
@@ -100,18 +115,17 @@ class AnalyzingHiC3DeFDR(object):
         self.save_data(disp_idx, 'disp_idx', chrom)
 
     # ------------------------------------------------------------------
-    def _f_and_dist(self):
-        """raw/f/dist of the disp pixels, all chromosomes concatenated
-        (reference ``analysis.py:169-183``)."""
-        disp_idx, disp_idx_offsets = self.load_data('disp_idx', 'all')
-        row, offsets = self.load_data('row', 'all', idx=disp_idx)
-        col, _ = self.load_data('col', 'all', idx=disp_idx)
-        raw, _ = self.load_data('raw', 'all', idx=disp_idx)
-        dist = col - row
-        f = np.ones_like(raw, dtype=float)
-        for i, chrom in enumerate(self.chroms):
-            sl = slice(offsets[i], offsets[i + 1])
-            di = disp_idx[disp_idx_offsets[i]:disp_idx_offsets[i + 1]]
+    def _f_and_dist(self, chroms=None):
+        """raw/f/dist of the disp pixels of ``chroms`` (default all),
+        concatenated in chromosome order (reference ``analysis.py:169-183``),
+        and the offsets between the chromosomes."""
+        chroms = self.chroms if chroms is None else chroms
+        raws, fs, dists = [], [], []
+        for chrom in chroms:
+            di = self.load_data('disp_idx', chrom)
+            row = self.load_data('row', chrom, idx=di)
+            col = self.load_data('col', chrom, idx=di)
+            raws.append(self.load_data('raw', chrom, idx=di))
             bias = self.load_bias(chrom)
             sf = self.load_data('size_factors', chrom)
             # per-replicate (1-D) factors of the non-conditional norms
@@ -120,18 +134,54 @@ class AnalyzingHiC3DeFDR(object):
             # (analysis.py:181) and raises IndexError.
             if sf.ndim == 2:
                 sf = sf[di]
-            f[sl] = bias[row[sl], :] * bias[col[sl], :] * sf
-        return raw, f, dist, offsets
+            fs.append(bias[row, :] * bias[col, :] * sf)
+            dists.append(col - row)
+        R = self.design.shape[0]
+        offsets = np.concatenate([[0], np.cumsum([len(r) for r in raws])])
+        if not raws:
+            return (np.zeros((0, R), dtype=np.int64), np.zeros((0, R)),
+                    np.zeros(0, dtype=np.int32), offsets)
+        return np.concatenate(raws), np.concatenate(fs), \
+            np.concatenate(dists), offsets
+
+    def _disp_per_dist_sharded(self, sh, raw, f, dist, C, D):
+        """estimate_disp's per-(distance, condition) qcml over every rank's
+        pixels: this rank's pixels on its GPU, the NLL sums of each data pass
+        all-reduced across ranks (parallel.make_allreduce) on torch's stream,
+        so every rank ends with the same disp_per_dist."""
+        import torch
+        ctx = self._ctx()
+        dev = torch.device('cuda', ctx.device)
+        torch.cuda.set_device(dev)
+        t_raw = torch.from_numpy(np.ascontiguousarray(
+            raw, dtype=np.int32)).to(dev)
+        t_f = torch.from_numpy(np.ascontiguousarray(f)).to(dev)
+        t_d = torch.from_numpy(np.ascontiguousarray(dist, dtype=np.int32)).to(dev)
+        torch.cuda.synchronize(dev)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        try:
+            return ctx.disp_per_dist_dev(
+                t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
+                self.design.shape[0], self._cond_of_rep(), C, D,
+                reduce=parallel.make_allreduce())
+        finally:
+            ctx.set_stream(None)
 
     def estimate_disp(self, estimator='qcml', frac=None, auto_frac_factor=15.,
                       weighted_lowess=True, n_threads=-1):
         """Reference ``analysis.py:135-223``."""
         eprint('estimating dispersion')
-        raw, f, dist, offsets = self._f_and_dist()
+        sh = self._shards()
+        raw, f, dist, offsets = self._f_and_dist(sh.mine)
         design = np.asarray(self.design, dtype=bool)
         C = design.shape[1]
         D = self.dist_thresh_max + 1
-        if callable(estimator):
+        if sh.sharded:
+            if estimator not in NATIVE_ESTIMATORS:
+                raise NotImplementedError(
+                    'sharded estimate_disp implements %s' % (NATIVE_ESTIMATORS,))
+            disp_per_dist = self._disp_per_dist_sharded(sh, raw, f, dist, C, D)
+        elif callable(estimator):
             # a user-supplied Python estimator runs where the user wrote it
             disp_per_dist = np.zeros((D, C))
             for c in range(C):
@@ -156,19 +206,25 @@ class AnalyzingHiC3DeFDR(object):
                                      auto_frac_factor=auto_frac_factor)
         for c, cond in enumerate(self.design.columns):
             table = tables[:, c]
-            fn = DispFn(table, disp_per_dist[:, c], weighted=weighted_lowess)
             disp[:, c] = table[dist]
-            self.save_disp_fn(cond, fn)
+            if sh.rank == 0:
+                self.save_disp_fn(cond, DispFn(table, disp_per_dist[:, c],
+                                               weighted=weighted_lowess))
         eprint('  saving estimated dispersions to disk')
-        self.save_data(disp, 'disp', offsets)
-        self.save_data(disp_per_dist, 'disp_per_dist')
+        for i, chrom in enumerate(sh.mine):
+            self.save_data(disp[offsets[i]:offsets[i + 1]], 'disp', chrom)
+        if sh.rank == 0:
+            self.save_data(disp_per_dist, 'disp_per_dist')
+        sh.barrier()
 
     # ------------------------------------------------------------------
     def lrt(self, chrom=None, refit_mu=True, n_threads=-1, verbose=True):
         """Reference ``analysis.py:225-284``."""
         if chrom is None:
-            for c in self.chroms:
+            sh = self._shards()
+            for c in sh.mine:
                 self.lrt(chrom=c, refit_mu=refit_mu, verbose=verbose)
+            sh.barrier()
             return
         eprint('running LRT for chrom %s' % chrom, skip=not verbose)
         bias = self.load_bias(chrom)
@@ -195,6 +251,18 @@ class AnalyzingHiC3DeFDR(object):
     def bh(self):
         """Reference ``analysis.py:286-303``."""
         eprint('applying BH-FDR correction')
+        sh = self._shards()
+        if sh.sharded:
+            mine = {}
+            for chrom in sh.mine:
+                li = self.load_data('loop_idx', chrom) \
+                    if self.loop_patterns else None
+                mine[chrom] = self.load_data('pvalues', chrom, idx=li)
+            for chrom, q in parallel.distributed_bh(sh, mine,
+                                                    _native.bh).items():
+                self.save_data(q, 'qvalues', chrom)
+            sh.barrier()
+            return
         loop_idx = self.load_data('loop_idx', 'all')[0] \
             if self.loop_patterns else None
         pvalues, offsets = self.load_data('pvalues', 'all', idx=loop_idx)

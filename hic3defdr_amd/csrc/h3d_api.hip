@@ -113,46 +113,35 @@ int work_grid(h3d_ctx* ctx, K kernel, size_t max_items) {
   return (int)std::max<size_t>(1, std::min<size_t>(max_items, (size_t)ctx->n_cu * nb));
 }
 
-template <int M>
+template <int M, bool NLL>
 void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                       const double* f_s, double* pd, int64_t n,
                       const int64_t* cs, const int32_t* cl, const int32_t* cd,
                       int C, const int32_t* rep_idx, const int32_t* n_rep,
                       const SegState* st, int* seg_flags, const int32_t* list,
                       const int32_t* meta, double* partial) {
-  // equalize pass (heavy: q2qnbinom), then the NLL-only pass (light)
+  // equalize pass (heavy: q2qnbinom), then (multi-rank driver) the NLL-only
+  // pass (light)
   {
     ProfScope ps(ctx, "disp_work", 0, 1);
-    bool done = false;
+#define H3D_EQ(WW)                                                                  \
+  do {                                                                              \
+    auto k = k_disp_work<M, WW, kEqualize, NLL>;                                    \
+    hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,      \
+                       ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, \
+                       st, seg_flags, list, meta, partial);                         \
+  } while (0)
     if constexpr (M == 4) {
-      done = true;
-      if (ctx->disp_w == 4) {
-        auto k = k_disp_work<M, 4, kEqualize>;
-        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
-                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
-                           n_rep, st, seg_flags, list, meta, partial);
-      } else if (ctx->disp_w == 3) {
-        auto k = k_disp_work<M, 3, kEqualize>;
-        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
-                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
-                           n_rep, st, seg_flags, list, meta, partial);
-      } else if (ctx->disp_w == 2) {
-        auto k = k_disp_work<M, 2, kEqualize>;
-        hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
-                           ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx,
-                           n_rep, st, seg_flags, list, meta, partial);
-      } else {
-        done = false;
-      }
+      if (ctx->disp_w == 4) H3D_EQ(4);
+      else if (ctx->disp_w == 3) H3D_EQ(3);
+      else if (ctx->disp_w == 2) H3D_EQ(2);
+      else H3D_EQ(1);
+    } else {
+      H3D_EQ(1);
     }
-    if (!done) {
-      auto k = k_disp_work<M, 1, kEqualize>;
-      hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
-                         ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                         st, seg_flags, list, meta, partial);
-    }
+#undef H3D_EQ
   }
-  {
+  if constexpr (NLL) {
     ProfScope ps(ctx, "disp_nll", 0);
     auto k = k_disp_work<M, 1, kNll>;
     if constexpr (M == 4) {
@@ -163,6 +152,25 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
                        st, seg_flags, list, meta, partial);
   }
+}
+
+// the whole Brent search of every freshly equalized segment (single rank)
+template <int M>
+void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_start,
+                  int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
+                  SegState* st, const int* seg_flags, double* result, int* queue) {
+  ProfScope ps(ctx, "disp_nll", 0);
+  auto k = k_brent<M>;
+  int& nb = ctx->resident[(const void*)k];
+  if (nb == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBrentBlock, 0) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+  }
+  const int grid = std::max(1, std::min(S, ctx->n_cu * nb));
+  (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), 0, ctx->stream, pd, n, seg_start, S,
+                     C, rep_idx, n_rep, st, seg_flags, result, queue, ctx->work_count);
 }
 
 // algorithmic HBM bytes of the disp_work launches so far: an equalize
@@ -472,33 +480,79 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                      d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
   if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 16, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
+  const int mslot = maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32;
   int rounds = 0, batch = 2, rc = 0;
-  while (true) {
+  if (!reduce) {
+    // Single rank: one equalize pass per qcml iteration over every segment
+    // that needs one, then k_brent runs each such segment's whole Brent
+    // search in-kernel, then k_seg_update rebuilds the equalize list. The
+    // host polls the live-segment count every `batch` iterations (an
+    // iteration with nothing to do costs three empty launches).
+    int* d_queue = (int*)scratch(ctx, "brent_queue", sizeof(int));
+    int64_t* d_seg = (int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
+    if (!d_queue || !d_seg) return fail(H3D_ENOMEM, "brent scratch");
+    if (n == 0) HIP_TRY(hipMemsetAsync(d_seg, 0, (D + 1) * 8, s));
+    batch = 3;
+    while (true) {
+      for (int b = 0; b < batch; ++b) {
+#define H3D_QCML_ITER(MM)                                                                 \
+  launch_disp_work<MM, false>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C,     \
+                              d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial); \
+  launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
+        if (mslot == 4) { H3D_QCML_ITER(4); }
+        else if (mslot == 8) { H3D_QCML_ITER(8); }
+        else if (mslot == 16) { H3D_QCML_ITER(16); }
+        else { H3D_QCML_ITER(32); }
+#undef H3D_QCML_ITER
+        {
+          ProfScope ps(ctx, "disp_update", 0);
+          hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
+                             d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
+                             d_res, d_meta, 0, 0, d_lpx, ctx->work_count);
+        }
+        ++rounds;
+      }
+      if (hipMemcpyAsync(h_meta, d_meta, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(hipGetLastError()));
+        break;
+      }
+      if (std::getenv("H3D_DEBUG"))
+        fprintf(stderr, "[h3d] qcml iterations=%d live_segments=%d\n", rounds, h_meta[3]);
+      if (h_meta[3] == 0) break;
+      if (rounds > 2000) {
+        rc = fail(H3D_ENOCONV, "estimate_disp did not terminate");
+        break;
+      }
+      batch = 2;
+    }
+  }
+  while (reduce && !rc) {
     for (int b = 0; b < batch; ++b) {
       {
-        switch (maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32) {
+        switch (mslot) {
           case 4:
-            launch_disp_work<4>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<4, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           case 8:
-            launch_disp_work<8>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<8, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           case 16:
-            launch_disp_work<16>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<16, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
           default:
-            launch_disp_work<32>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            launch_disp_work<32, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
         }
       }
       {
         ProfScope ps(ctx, "disp_reduce", 0);
-        // single rank: the reduce kernel steps the state machines too; with
-        // a cross-rank all-reduce in between, k_seg_update steps them
+        // this rank's per-segment sums; the cross-rank all-reduce follows and
+        // k_seg_update steps the (identical) state machines
         hipLaunchKernelGGL(k_seg_reduce, dim3((S + 3) / 4), dim3(256), 0, s,
-                           d_partial, d_slb, d_sle, S, d_total,
-                           reduce ? nullptr : d_st, d_flags, d_nrep, C, d_res);
+                           d_partial, d_slb, d_sle, S, d_total, nullptr, d_flags,
+                           d_nrep, C, d_res);
       }
-      if (reduce && reduce(d_total, S, user)) {
+      if (reduce(d_total, S, user)) {
         rc = fail(H3D_EHIP, "allreduce callback failed");
         break;
       }
@@ -506,7 +560,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         ProfScope ps(ctx, "disp_update", 0);
         hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                            d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb,
-                           d_sle, d_res, d_meta, 0, reduce ? 1 : 0, d_lpx, ctx->work_count);
+                           d_sle, d_res, d_meta, 0, 1, d_lpx, ctx->work_count);
       }
       ++rounds;
     }

@@ -23,6 +23,7 @@ namespace h3d {
 constexpr int kChunk = 256;  // pixels per disp work item (= block size)
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / 64;  // disp partials per work item
+constexpr int kBrentBlock = 512;  // k_brent: one workgroup per segment
 
 // deterministic wave sum (fixed butterfly); result valid in every lane
 __device__ inline double wave_sum(double v) {
@@ -161,7 +162,10 @@ __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
 // the equalize items first (meta[2] of them), then the NLL items, and each
 // pass is its own kernel so the light NLL pass is not held to the register
 // budget of q2qnbinom. W = minimum waves per SIMD asked of the allocator.
-template <int M, int W, int PH>
+// NLL = false (single-rank driver): the equalize pass only writes the
+// pseudodata; k_brent then evaluates every NLL of the segment's Brent search
+// in one workgroup.
+template <int M, int W, int PH, bool NLL = true>
 __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int32_t* __restrict__ raw_s, const double* __restrict__ f_s,
     double* __restrict__ pd, int64_t n, const int64_t* __restrict__ chunk_start,
@@ -243,6 +247,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           pd[o] = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
         }
       }
+      if constexpr (!NLL) continue;
       // NLL term in replicate order (numpy's row sum) over the pseudodata
       // (in the equalize pass: the values this thread just wrote). All loads
       // are issued up front into the slot registers; the rolled loop then
@@ -287,6 +292,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
 #pragma unroll
         for (int k = 0; k < M; ++k)
           if (k < nr) pd[(int64_t)ri[k] * n + px] = d[k];
+        if constexpr (!NLL) continue;
       } else {
 #pragma unroll
         for (int k = 0; k < M; ++k)
@@ -297,8 +303,10 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     }
     // one partial per wave (fixed shuffle tree -> deterministic); no block
     // barrier, so the waves of a block run their items independently
-    const double t = wave_sum(term);
-    if ((threadIdx.x & 63) == 0) partial[(int64_t)w * kWavesPerBlock + (threadIdx.x >> 6)] = t;
+    if constexpr (NLL) {
+      const double t = wave_sum(term);
+      if ((threadIdx.x & 63) == 0) partial[(int64_t)w * kWavesPerBlock + (threadIdx.x >> 6)] = t;
+    }
   }
 }
 
@@ -478,6 +486,101 @@ __global__ __launch_bounds__(1024) void k_seg_update(
     // rank's own list length meta[1]) is the same on every rank and is what
     // the host loop terminates on
     meta[3] = live_total;
+  }
+}
+
+// The whole bounded-Brent search of cml (dispersion.py:46-80) for every
+// segment whose pseudodata the equalize pass just wrote (phase kEqualize):
+// one workgroup per segment (taken from a device queue), every NLL
+// evaluation in-kernel over the segment's pseudodata (contiguous in the
+// distance-sorted SoA, L2/MALL-resident across the evaluations), a fixed-order
+// block reduction per evaluation (deterministic), and the state machine
+// stepped by every thread on the same total (uniform, no broadcast). Exits
+// when the segment needs its next equalize pass (next qcml iteration) or is
+// done; seg_step bounds the loop (500 Brent evaluations -> kFlagBrentFail).
+// The NLL work is compute-bound (lgamma); measured r02 on cfg2 against a
+// dynamically scheduled variant (persistent workgroups draining a device
+// ring of (segment, 2048-pixel chunk) tasks with agent-scope hand-offs):
+// 4.6 vs 6.4 ms per step -- the per-task acquire and arrival traffic cost
+// more than the tail the static grid leaves idle.
+// seg_step out of line for k_brent: run by one thread once per evaluation,
+// its registers stay out of the NLL loop's budget
+__device__ __noinline__ void seg_step_ool(SegState* s, double total, int n_reps) {
+  seg_step(s, total, n_reps);
+}
+
+template <int M>
+__global__ __launch_bounds__(kBrentBlock, 4) void k_brent(
+    const double* __restrict__ pd, int64_t n,
+    const int64_t* __restrict__ seg_start /* D + 1 */, int S, int C,
+    const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
+    const int32_t* __restrict__ n_rep /* C */, SegState* __restrict__ st,
+    const int* __restrict__ seg_flags, double* __restrict__ result,
+    int* __restrict__ queue, unsigned long long* __restrict__ work_count) {
+  // the state machine lives in LDS and is stepped by thread 0; the data loop
+  // only holds the four NLL constants (the SegState in every thread's VGPRs
+  // spilled at the 1024-thread register budget)
+  __shared__ SegState s_st;
+  __shared__ double wpart[kBrentBlock / 64];
+  __shared__ int s_next, s_more;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  while (true) {
+    __syncthreads();  // s_next / s_st reuse
+    if (threadIdx.x == 0) s_next = atomicAdd(queue, 1);
+    __syncthreads();
+    const int s = s_next;
+    if (s >= S) break;
+    if (st[s].phase != kEqualize) continue;  // done, or nothing to search
+    if (threadIdx.x == 0) {
+      s_st = st[s];
+      s_st.flags |= seg_flags[s];
+    }
+    const int d = s / C, c = s - (s / C) * C;
+    const int nr = n_rep[c];
+    const int64_t b = seg_start[d], e = seg_start[d + 1];
+    int ri[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) ri[k] = (k < nr) ? rep_idx[c * kMaxReps + k] : 0;
+    int evals = 0;
+    __syncthreads();
+    while (true) {
+      const NllConst kc = s_st.k;
+      double acc = 0.0;
+      // next pixel's pseudodata loaded one iteration ahead (latency hidden
+      // behind the current pixel's lgammas)
+      int64_t px = b + threadIdx.x;
+      double v[M];
+#pragma unroll
+      for (int k = 0; k < M; ++k) v[k] = (k < nr && px < e) ? pd[(int64_t)ri[k] * n + px] : 0.0;
+      for (; px < e; px += kBrentBlock) {
+        const int64_t nx = px + kBrentBlock;
+        double w[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) w[k] = (k < nr && nx < e) ? pd[(int64_t)ri[k] * n + nx] : 0.0;
+        acc += nll_pixel<M>(v, nr, kc);
+#pragma unroll
+        for (int k = 0; k < M; ++k) v[k] = w[k];
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) wpart[wid] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double total = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBrentBlock / 64; ++w) total += wpart[w];
+        seg_step_ool(&s_st, total, nr);
+        s_more = (s_st.phase == kNll) ? 1 : 0;
+      }
+      ++evals;
+      __syncthreads();  // s_st / s_more / wpart
+      if (!s_more) break;
+    }
+    if (threadIdx.x == 0) {
+      st[s] = s_st;
+      if (s_st.phase == kDone) result[s] = s_st.result;
+      atomicAdd(&work_count[1], (unsigned long long)(e - b) * nr * evals);
+    }
   }
 }
 

@@ -192,13 +192,23 @@ H3D_HD double lgam_cached(double a, LgamCache* c) {
   return c->lga;
 }
 
+// q2qnbinom's arithmetic on already clamped means (mi, mo), with lgam of the
+// output gamma shape either given (lga_out) or taken from `cache` (lga_out
+// NaN).
+H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
+                       double lga_out, LgamCache* cache);
+
 H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha,
                   LgamCache* cache = nullptr) {
   if (!((*mu_in >= 0.25) && (*mu_out >= 0.25))) {
     *mu_in = 0.25;
     *mu_out = 0.25;
   }
-  const double mi = *mu_in, mo = *mu_out;
+  return q2q_core(x, *mu_in, *mu_out, alpha, NAN, cache);
+}
+
+H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
+                       double lga_out, LgamCache* cache) {
   const double r_in = 1 + alpha * mi, r_out = 1 + alpha * mo;
   const double v_in = mi * r_in, v_out = mo * r_out;
   const double sd_in = sqrt(v_in), sd_out = sqrt(v_out);
@@ -253,7 +263,8 @@ H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha,
       const double y = m_out + zz / sqrt(9.0 * a_out);
       if (y > 0.0) guess = a_out * y * y * y;
     }
-    qg = igam_inv(a_out, tg, right, lgam_cached(a_out, cache), guess) * r_out;
+    const double lga = (lga_out == lga_out) ? lga_out : lgam_cached(a_out, cache);
+    qg = igam_inv(a_out, tg, right, lga, guess) * r_out;
   }
   double pc = (qn + qg) / 2;
   if (!(pc >= 0.0)) pc = 0.0;
@@ -391,13 +402,31 @@ H3D_HD NllConst nll_const(double delta, int n) {
 // - n gammaln(r); nll(delta) = -(sum over pixels). The per-pixel gammaln
 // terms use lgam_nll (absolute error ~1e-15, far below the rounding of the
 // segment sum), the per-segment constants cephes lgam.
+//
+// The shift products of the R_c + 1 lgammas are folded into one logarithm
+// per 8 replicates (lgam_nll_parts): ln(prod P_j / P_z) -- the products stay
+// far inside the double range (P < 15^10 per factor, >= ~1e-2) -- which
+// halves the transcendental work of the NLL passes. Arguments: d_j + r >=
+// 1/101 - ... > 0 (r = 1/delta - 1 >= 1/0.99 - 1, pseudodata >= 0).
 template <int M>
 H3D_HD double nll_pixel(const double* d, int n, const NllConst& k) {
   double lg[M];
+  double lnp = 0.0, prod = 1.0;
 #pragma unroll
-  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam_nll(d[j] + k.r) : 0.0;
+  for (int j = 0; j < M; ++j) {
+    double pj = 1.0;
+    lg[j] = (j < n) ? lgam_nll_parts(d[j] + k.r, &pj) : 0.0;
+    prod *= pj;
+    if ((j & 7) == 7 && j + 1 < M) {  // keep 8 factors per logarithm
+      lnp += log_fast(prod);
+      prod = 1.0;
+    }
+  }
   const double z = np_sum<M>(d, n);
-  return np_sum<M>(lg, n) + k.lg_nr - lgam_nll(z + k.nr) - k.n_lg_r;
+  double pz = 1.0;
+  const double lz = lgam_nll_parts(z + k.nr, &pz);
+  lnp += log_fast(prod * recip_nll(pz));
+  return np_sum<M>(lg, n) - lnp + k.lg_nr - lz - k.n_lg_r;
 }
 
 // ---- qcml + bounded Brent as a resumable state machine --------------------

@@ -141,11 +141,24 @@ H3D_HD double lgam(double x) {
   return q;
 }
 
+// 1/y for the NLL lgamma (absolute accuracy): on gfx950 v_rcp_f64 + one
+// Newton step (~1 ulp) instead of the IEEE division sequence; the host
+// build divides.
+H3D_HD double recip_nll(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double r0 = __builtin_amdgcn_rcp(y);
+  return fma(fma(-y, r0, 1.0), r0, r0);
+#else
+  return 1.0 / y;
+#endif
+}
+
 // Natural log for finite x > 0 in straight-line code: x = m 2^e with
 // m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh(s), s = (m - 1) / (m + 1),
 // |s| <= 0.1716, by 11 terms of the atanh series (truncation < 1e-18).
 // Error ~2 ulp of ln m plus the rounding of e ln 2 -- a few 1e-16 relative,
-// at about half the instructions of the libm-accurate log.
+// at about half the instructions of the libm-accurate log (on gfx950 the
+// quotient uses recip_nll: one more ulp). Used by the NLL sums only.
 H3D_HD double log_fast(double x) {
 #if defined(__clang__)
 #pragma clang fp contract(fast)  // used by the NLL lgamma only (see there)
@@ -156,7 +169,7 @@ H3D_HD double log_fast(double x) {
     m *= 2.0;
     e -= 1;
   }
-  const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+  const double s = (m - 1.0) * recip_nll(m + 1.0), s2 = s * s;
   double p = 1.0 / 21.0;
   p = p * s2 + 1.0 / 19.0;
   p = p * s2 + 1.0 / 17.0;
@@ -204,7 +217,7 @@ H3D_HD double lgam_nll(double x) {
     P = two ? px * pu : pu;
     y = u + 5.0;
   }
-  const double r = 1.0 / y, r2 = r * r;
+  const double r = recip_nll(y), r2 = r * r;
   const double corr =
       r * (1.0 / 12.0 +
            r2 * (-1.0 / 360.0 +
@@ -217,6 +230,37 @@ H3D_HD double lgam_nll(double x) {
   double v = (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
   if (x < 10.0) v -= log_fast(P);
   return v;
+}
+
+// lgam_nll split for batching: returns lgam(x) + ln P and sets *P, the
+// shift product (1 for x >= 10), so a caller summing several lgammas takes
+// ONE log of the combined product (nll_pixel: per pixel R_c + 1 lgammas, one
+// ln P instead of up to R_c + 1).
+H3D_HD double lgam_nll_parts(double x, double* P) {
+#if defined(__clang__)
+#pragma clang fp contract(fast)
+#endif
+  double y = x, p = 1.0;
+  if (x < 10.0) {
+    const bool two = x < 5.0;
+    const double u = two ? x + 5.0 : x;
+    const double pu = ((((u + 10.0) * u + 35.0) * u + 50.0) * u + 24.0) * u;
+    const double px = ((((x + 10.0) * x + 35.0) * x + 50.0) * x + 24.0) * x;
+    p = two ? px * pu : pu;
+    y = u + 5.0;
+  }
+  *P = p;
+  const double r = recip_nll(y), r2 = r * r;
+  const double corr =
+      r * (1.0 / 12.0 +
+           r2 * (-1.0 / 360.0 +
+                 r2 * (1.0 / 1260.0 +
+                       r2 * (-1.0 / 1680.0 +
+                             r2 * (1.0 / 1188.0 +
+                                   r2 * (-691.0 / 360360.0 +
+                                         r2 * (1.0 / 156.0 +
+                                               r2 * (-3617.0 / 122400.0))))))));
+  return (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
 }
 
 // log(1 + x) - x (cephes log1pmx). For |x| < 0.5 cephes sums the Taylor

@@ -1,0 +1,38 @@
+"""torchrun worker for tests/test_gpu_dist.py: the product's sharded
+HiC3DeFDR.run_to_qvalues() on a golden dataset, one rank per process, every
+rank on the GPU H3D_DEVICE names, backend gloo (several ranks on one GPU;
+RCCL refuses duplicate devices).
+
+    torchrun --nproc-per-node 2 tests/dist_product_main.py <name> <outdir>
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    import pandas as pd
+    import torch.distributed as dist
+    from conftest import e2e_inputs
+    from hic3defdr_amd import HiC3DeFDR
+    name, outdir = sys.argv[1], sys.argv[2]
+    dist.init_process_group('gloo')
+    _, kw = e2e_inputs(name)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir,
+                  dist_thresh_max=kw['dist_thresh_max'],
+                  loop_patterns=kw['loop_patterns'], res=10000)
+    sh = h._shards()
+    print('rank %d of %d owns %s' % (sh.rank, sh.world, sh.mine), flush=True)
+    h.run_to_qvalues(verbose=False)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

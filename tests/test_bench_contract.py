@@ -1,6 +1,7 @@
-"""bench.py host-side contract (no GPU): the roofline traffic figure comes
-from the committed PMC summary of the default command and only for that
-workload; the LRT byte count matches DESIGN.md's 108 B/px at R=4, C=2."""
+"""bench.py host-side contract (no GPU): the roofline figures that need
+hardware counters come from the committed PMC summary of the default
+command, and only for that workload; the LRT byte count matches DESIGN.md's
+108 B/px at R=4, C=2."""
 import json
 import os
 import sys
@@ -15,18 +16,28 @@ def test_pmc_summary_matches_default_workload():
     d = json.load(open(bench.PMC_SUMMARY))
     assert (d['bins'], d['dmax']) == (20000, 250)
     names = [k.split('[')[0] for k in d['kernels']]
-    assert any('k_disp_work<4, 4, 0>' in k for k in names)
+    for kern in ('k_disp_work<4, 4, 0, false>', 'k_brent<4>', 'k_lrt<4, 2>'):
+        assert any(kern in k for k in names), kern
 
 
-def test_pmc_traffic_per_launch():
-    t = bench.pmc_traffic('k_disp_work<4, 4, 0>', 20000, 250)
+def test_pmc_kernel_per_launch():
     d = json.load(open(bench.PMC_SUMMARY))
-    e = [v for k, v in d['kernels'].items() if 'k_disp_work<4, 4, 0>' in k][0]
-    want = (e['hbm_read_bytes_corrected'] + e['hbm_write_bytes']) / e['dispatches']
-    assert t == want and t > 0
-    # other workloads were not profiled: traffic stays null
-    assert bench.pmc_traffic('k_disp_work<4, 4, 0>', 1000, 250) is None
-    assert bench.pmc_traffic('no_such_kernel', 20000, 250) is None
+    t = bench.pmc_kernel('k_disp_work<4, 4, 0, false>', 20000, 250)
+    es = [v for k, v in d['kernels'].items() if 'k_disp_work<4, 4, 0, false>' in k]
+    n = sum(e['dispatches'] for e in es)
+    want = sum(e['hbm_read_bytes_corrected'] + e['hbm_write_bytes']
+               for e in es) / n
+    assert abs(t['hbm_bytes'] - want) <= 1e-9 * want and want > 0
+    fl = sum(64 * (e['SQ_INSTS_VALU_ADD_F64'] + e['SQ_INSTS_VALU_MUL_F64'] +
+                   e['SQ_INSTS_VALU_TRANS_F64'] +
+                   2 * e['SQ_INSTS_VALU_FMA_F64']) for e in es) / n
+    assert abs(t['f64_flops'] - fl) <= 1e-9 * fl and fl > 0
+    assert 0 < t['lane_util'] <= 1
+    # other workloads were not profiled: the counter figures stay null
+    assert bench.pmc_kernel('k_disp_work<4, 4, 0, false>', 1000, 250) is None
+    assert bench.pmc_kernel('no_such_kernel', 20000, 250) is None
+    r = bench.fp64_roof(t, 1e-3)
+    assert abs(r['frac'] - t['f64_flops'] / 1e-3 / 1e12 / 78.6) < 1e-12
 
 
 def test_lrt_bytes_per_pixel():

@@ -112,3 +112,48 @@ def test_sharded_disp_equals_single_rank_and_oracle():
         _, dpd, _ = oracle.estimate_disp(preps, biases, kw['design'],
                                          dist_thresh_max=D - 1)
         np.testing.assert_allclose(sharded, dpd, rtol=1e-6, atol=1e-12)
+
+
+def _bh_worker(rank, world, port, chroms, pv, result_file):
+    """Product orchestration on gloo: Shards (LPT over the chromosomes) and
+    the genome-wide BH gather (rank 0) / scatter (parallel.distributed_bh)."""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    sh = parallel.Shards(chroms, {c: len(pv[c]) for c in chroms})
+    assert sh.sharded and sh.world == world
+    q = parallel.distributed_bh(sh, {c: pv[c] for c in sh.mine},
+                                oracle.adjust_pvalues)
+    assert sorted(q) == sorted(sh.mine)
+    np.save(result_file % rank, np.array([sh.mine, [q[c] for c in sh.mine]],
+                                         dtype=object), allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_bh_equals_single_process():
+    rng = np.random.default_rng(3)
+    chroms = ['chr1', 'chr2', 'chr10', 'chrX', 'chrY']
+    pv = {c: rng.uniform(0, 1, int(rng.integers(5, 300))) ** 3 for c in chroms}
+    pv['chr2'][::7] = np.nan   # NaN p-values stay NaN, are not counted
+    world = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        res = os.path.join(tmp, 'q%d.npy')
+        port = 29700 + (os.getpid() % 1000)
+        mp.spawn(_bh_worker, args=(world, port, chroms, pv, res), nprocs=world,
+                 join=True)
+        got = {}
+        for r in range(world):
+            mine, qs = np.load(res % r, allow_pickle=True)
+            got.update(dict(zip(mine, qs)))
+    assert sorted(got) == sorted(chroms)
+    allq = oracle.adjust_pvalues(np.concatenate([pv[c] for c in chroms]))
+    off = np.concatenate([[0], np.cumsum([len(pv[c]) for c in chroms])])
+    for i, c in enumerate(chroms):
+        np.testing.assert_array_equal(got[c], allq[off[i]:off[i + 1]])
+
+
+def test_shards_single_process_owns_everything():
+    sh = parallel.Shards(['a', 'b', 'c'])
+    assert not sh.sharded and sh.mine == ['a', 'b', 'c'] and sh.rank == 0

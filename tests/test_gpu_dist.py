@@ -1,0 +1,58 @@
+"""Multi-rank product on the GPU: HiC3DeFDR.run_to_qvalues() under torchrun
+with 2 ranks on cuda:0 (gloo on device tensors), launched as fresh child
+processes. Every chromosome is prepared and tested by the rank LPT assigns
+it, estimate_disp runs the device driver's multi-rank branch (per-pass
+all-reduce of the NLL sums through parallel.make_allreduce on torch's
+stream), BH gathers on rank 0 and scatters back. The outdir must match the
+reference goldens like the single-rank run does (tests/test_gpu_e2e.py)."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import REPO, e2e_inputs, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('name', ['small2'])
+def test_two_ranks_run_to_qvalues_matches_reference(name):
+    g, kw = e2e_inputs(name)
+    assert len(kw['chroms']) == 2   # one chromosome per rank
+    outdir = tempfile.mkdtemp(prefix='h3d_dist_')
+    try:
+        env = dict(os.environ, H3D_DEVICE='0', MASTER_ADDR='127.0.0.1',
+                   OMP_NUM_THREADS='1')
+        port = 29600 + os.getpid() % 1000
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+               '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+               '--master-port', str(port),
+               os.path.join(REPO, 'tests', 'dist_product_main.py'), name,
+               outdir]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        owned = sorted(l for l in r.stdout.splitlines() if 'owns' in l)
+        assert len(owned) == 2 and "['chrA']" in ' '.join(owned) and \
+            "['chrB']" in ' '.join(owned), owned
+        dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
+        np.testing.assert_allclose(dpd, g['disp_per_dist'], rtol=1e-6,
+                                   atol=1e-12)
+        for c in kw['chroms']:
+            def ld(st):
+                return np.load(os.path.join(outdir, '%s_%s.npy' % (st, c)))
+            for st in ('row', 'col', 'raw', 'disp_idx', 'loop_idx'):
+                np.testing.assert_array_equal(ld(st), g['%s__%s' % (st, c)])
+            for st, tol in (('disp', 1e-6), ('pvalues', 1e-6),
+                            ('qvalues', 1e-6), ('mu_hat_null', 1e-8),
+                            ('mu_hat_alt', 1e-8)):
+                assert rel_err(ld(st), g['%s__%s' % (st, c)]) < tol, st
+            for fdr in (0.01, 0.05, 0.1):
+                np.testing.assert_array_equal(ld('qvalues') < fdr,
+                                              g['qvalues__%s' % c] < fdr)
+    finally:
+        shutil.rmtree(outdir, ignore_errors=True)

@@ -141,10 +141,11 @@ def test_disp_and_lrt_vs_oracle_larger(ctx):
 
 
 def test_disp_dev_with_noop_reduce_matches_single_rank(ctx):
-    """The multi-rank branch of the device driver (k_seg_reduce without the
-    state step, k_seg_update step=1, the reduce hook on the ctx stream,
-    termination on the live-segment count) with an identity all-reduce gives
-    the single-rank result bit for bit."""
+    """The multi-rank branch of the device driver (per-pass k_disp_work NLL
+    sums, k_seg_reduce, the reduce hook on the ctx stream, k_seg_update
+    step=1, termination on the live-segment count) with an identity
+    all-reduce vs the single-rank driver (k_brent): same dispersions, both
+    deterministic."""
     import torch
     from hic3defdr_amd import _native
     g, kw, raw, f, dist = _stage_inputs('small2')
@@ -163,9 +164,13 @@ def test_disp_dev_with_noop_reduce_matches_single_rank(ctx):
 
     args = (t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
             raw.shape[1], cond, C, D)
-    one = ctx.disp_per_dist_dev(*args)
+    one = ctx.disp_per_dist_dev(*args)      # in-kernel Brent (k_brent)
     multi = ctx.disp_per_dist_dev(*args, reduce=noop)
     assert len(calls) > 10
-    np.testing.assert_array_equal(one, multi)
+    again = ctx.disp_per_dist_dev(*args, reduce=noop)
+    np.testing.assert_array_equal(multi, again)   # deterministic
+    np.testing.assert_array_equal(one, ctx.disp_per_dist_dev(*args))
+    # the two drivers sum the NLL terms in different orders
+    np.testing.assert_allclose(one, multi, rtol=1e-7, atol=1e-12)
     np.testing.assert_allclose(multi, g['disp_per_dist'], rtol=RTOL_DISP,
                                atol=1e-12)

@@ -242,4 +242,6 @@ def test_lgam_nll_and_log_fast(lib):
     assert np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref))) < 1.2e-14
     assert np.isinf(unary(lib, 'lgam_nll', np.array([np.inf])))[0]
     v = 10 ** rng.uniform(-300, 300, 40000)
-    assert rel_err(unary(lib, 'log_fast', v), np.log(v)) < 4e-16
+    # the gfx950 build forms its quotient with v_rcp_f64 + one Newton step
+    # (one more ulp); the NLL sums need absolute accuracy only
+    assert rel_err(unary(lib, 'log_fast', v), np.log(v)) < 6e-16
