@@ -318,7 +318,11 @@ def main():
         t_mu1 = torch.empty((n, C), dtype=torch.float64, device=dev)
         t_disp = torch.empty_like(t_mu1)
         torch.cuda.synchronize()
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        # libh3d and the RCCL all-reduce share one real stream (torch's
+        # default stream has handle 0 = "the ctx's own stream" to libh3d)
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        ctx.set_stream(stream.cuda_stream)
         reduce = parallel.make_allreduce() if world > 1 else None
 
         def step():

@@ -158,13 +158,19 @@ class AnalyzingHiC3DeFDR(object):
         t_f = torch.from_numpy(np.ascontiguousarray(f)).to(dev)
         t_d = torch.from_numpy(np.ascontiguousarray(dist, dtype=np.int32)).to(dev)
         torch.cuda.synchronize(dev)
-        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        # a real stream shared by libh3d and the collective: torch's default
+        # stream has handle 0, which h3d_set_stream reads as "the ctx's own
+        # stream" -- the all-reduce would then race the kernels around it
+        stream = torch.cuda.Stream(dev)
+        ctx.set_stream(stream.cuda_stream)
         try:
-            return ctx.disp_per_dist_dev(
-                t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
-                self.design.shape[0], self._cond_of_rep(), C, D,
-                reduce=parallel.make_allreduce())
+            with torch.cuda.stream(stream):
+                return ctx.disp_per_dist_dev(
+                    t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
+                    self.design.shape[0], self._cond_of_rep(), C, D,
+                    reduce=parallel.make_allreduce())
         finally:
+            stream.synchronize()
             ctx.set_stream(None)
 
     def estimate_disp(self, estimator='qcml', frac=None, auto_frac_factor=15.,

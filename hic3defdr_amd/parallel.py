@@ -51,9 +51,11 @@ class _CudaArray(object):
 
 def make_allreduce(group=None):
     """``reduce(ptr, count)`` for ``Context.disp_per_dist_dev``: sums a
-    device buffer of doubles in place across ranks on the current stream.
-    The caller must run libh3d on torch's current stream
-    (``ctx.set_stream(torch.cuda.current_stream().cuda_stream)``)."""
+    device buffer of doubles in place across ranks on torch's current
+    stream. libh3d must launch on that same stream, and it must be a real
+    (non-default) stream: ``s = torch.cuda.Stream(); ctx.set_stream(
+    s.cuda_stream)`` under ``torch.cuda.stream(s)`` -- the default stream's
+    handle is 0, which h3d_set_stream takes as "the ctx's own stream"."""
     import torch
     import torch.distributed as dist
 

@@ -4,7 +4,11 @@ processes. Every chromosome is prepared and tested by the rank LPT assigns
 it, estimate_disp runs the device driver's multi-rank branch (per-pass
 all-reduce of the NLL sums through parallel.make_allreduce on torch's
 stream), BH gathers on rank 0 and scatters back. The outdir must match the
-reference goldens like the single-rank run does (tests/test_gpu_e2e.py)."""
+reference goldens like the single-rank run does (tests/test_gpu_e2e.py).
+
+The file sorts first so the pytest process has not touched the GPU when it
+starts the ranks (a GPU-initialised parent made the same launch stall on
+the box); the ranks' output goes to log files, not pipes."""
 import os
 import shutil
 import subprocess
@@ -26,17 +30,24 @@ def test_two_ranks_run_to_qvalues_matches_reference(name):
     outdir = tempfile.mkdtemp(prefix='h3d_dist_')
     try:
         env = dict(os.environ, H3D_DEVICE='0', MASTER_ADDR='127.0.0.1',
-                   OMP_NUM_THREADS='1')
+                   OMP_NUM_THREADS='1', H3D_DEBUG='1')
         port = 29600 + os.getpid() % 1000
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
                '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
                '--master-port', str(port),
                os.path.join(REPO, 'tests', 'dist_product_main.py'), name,
                outdir]
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True,
-                           timeout=240)
-        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-        owned = sorted(l for l in r.stdout.splitlines() if 'owns' in l)
+        log = os.path.join(outdir, 'ranks.log')
+        with open(log, 'w') as fh:
+            try:
+                rc = subprocess.run(cmd, env=env, stdout=fh,
+                                    stderr=subprocess.STDOUT,
+                                    timeout=150).returncode
+            except subprocess.TimeoutExpired:
+                rc = 'timeout'
+        text = open(log).read()
+        assert rc == 0, text[-4000:]
+        owned = sorted(l for l in text.splitlines() if 'owns' in l)
         assert len(owned) == 2 and "['chrA']" in ' '.join(owned) and \
             "['chrB']" in ' '.join(owned), owned
         dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
