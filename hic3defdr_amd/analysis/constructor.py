@@ -6,9 +6,10 @@ import pandas as pd
 
 from hic3defdr_amd.analysis.core import CoreHiC3DeFDR
 from hic3defdr_amd.analysis.analysis import AnalyzingHiC3DeFDR
+from hic3defdr_amd.analysis.simulation import SimulatingHiC3DeFDR
 
 
-class HiC3DeFDR(CoreHiC3DeFDR, AnalyzingHiC3DeFDR):
+class HiC3DeFDR(CoreHiC3DeFDR, AnalyzingHiC3DeFDR, SimulatingHiC3DeFDR):
     """Main object for a hic3defdr analysis (MI355X-native hot path).
 
     Same constructor as the reference (``constructor.py:62-86``):

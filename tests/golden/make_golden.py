@@ -592,10 +592,100 @@ def run_hard_cfg2(bins=20000, dmax=250, seed=0):
                         meta_seed=np.array(seed))
 
 
+SIM_EVALS = [(None, None, False), (None, 15, False), (16, 30, True),
+             (31, None, False)]
+
+
+def run_sim(name='small2', seed=0):
+    """simulate() -> filter + kr_balance (README.md:586-614) -> a new
+    analysis on the simulated replicates -> evaluate() (simulation.py,
+    util/simulation.py, util/balancing.py, util/filtering.py,
+    util/evaluation.py), all by the reference, on the committed small2
+    inputs. sim_<name>.npz: the cluster labels, every simulated CSR
+    replicate (data / indices / indptr), the balancing bias vectors, the
+    simulated analysis' p / q-values and disp_per_dist, every eval npz."""
+    import scipy.sparse as sp
+    from hic3defdr.util.balancing import kr_balance
+    from hic3defdr.util.filtering import filter_sparse_rows_count
+    sizes, dmax, npc, _, loops = E2E[name]
+    base = os.path.join(HERE, 'data', name)
+    g = np.load(os.path.join(HERE, 'e2e_%s.npz' % name))
+    reps = [str(r) for r in g['meta_reps']]
+    conds = [str(c) for c in g['meta_conds']]
+    chroms = [str(c) for c in g['meta_chroms']]
+    design = pd.DataFrame(g['meta_design'].astype(bool), index=reps,
+                          columns=conds)
+    lp = {c: os.path.join(base, 'clusters', '%s_<chrom>.json' % c)
+          for c in conds}
+    outdir = os.path.join('/tmp', 'h3golden_simsrc_' + name)
+    simdir = os.path.join('/tmp', 'h3golden_sim_' + name)
+    for d in (outdir, simdir):
+        shutil.rmtree(d, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=[os.path.join(base, r, '<chrom>_raw.npz')
+                                    for r in reps],
+                  bias_patterns=[os.path.join(base, r, '<chrom>_kr.bias')
+                                 for r in reps],
+                  chroms=chroms, design=design, outdir=outdir,
+                  dist_thresh_max=dmax, loop_patterns=lp)
+    h.run_to_qvalues(n_threads=0, verbose=False)
+    np.random.seed(seed)
+    h.simulate('ES', outdir=simdir, n_threads=0, verbose=False)
+    out = {'meta_seed': np.array(seed), 'meta_cond': np.array('ES'),
+           'meta_evals': np.array([[-1 if a is None else a,
+                                    -1 if b is None else b, int(rr)]
+                                   for a, b, rr in SIM_EVALS])}
+    simreps = ['A1', 'A2', 'B1', 'B2']
+    for chrom in chroms:
+        out['labels__%s' % chrom] = np.loadtxt(
+            os.path.join(simdir, 'labels_%s.txt' % chrom), dtype='U7')
+        for rep in simreps:
+            fn = os.path.join(simdir, '%s_%s_raw.npz' % (rep, chrom))
+            m = sp.load_npz(fn).tocsr()
+            for part in ('data', 'indices', 'indptr'):
+                out['sim__%s__%s__%s' % (rep, chrom, part)] = getattr(m, part)
+            filt = filter_sparse_rows_count(m)
+            fm = filt.tocsr()
+            out['filt__%s__%s__nnz' % (rep, chrom)] = np.array(fm.nnz)
+            out['filt__%s__%s__rowsum' % (rep, chrom)] = np.asarray(
+                fm.sum(axis=1)).ravel()
+            _, bias, _ = kr_balance(filt, fl=0)
+            out['bias__%s__%s' % (rep, chrom)] = bias
+            np.savetxt(fn.replace('_raw.npz', '_kr.bias'), bias)
+    out['sim_design_csv'] = np.frombuffer(
+        open(os.path.join(simdir, 'design.csv'), 'rb').read(), dtype=np.uint8)
+    simout = os.path.join('/tmp', 'h3golden_simout_' + name)
+    shutil.rmtree(simout, ignore_errors=True)
+    hs = HiC3DeFDR(
+        raw_npz_patterns=[os.path.join(simdir, '%s_<chrom>_raw.npz' % r)
+                          for r in simreps],
+        bias_patterns=[os.path.join(simdir, '%s_<chrom>_kr.bias' % r)
+                       for r in simreps],
+        chroms=chroms, design=os.path.join(simdir, 'design.csv'),
+        outdir=simout, dist_thresh_max=dmax, loop_patterns={'ES': lp['ES']})
+    hs.run_to_qvalues(n_threads=0, verbose=False)
+    for chrom in chroms:
+        for st in ('pvalues', 'qvalues', 'disp_idx', 'loop_idx', 'row',
+                   'col'):
+            out['simrun__%s__%s' % (st, chrom)] = np.load(
+                os.path.join(simout, '%s_%s.npy' % (st, chrom)))
+    out['simrun__disp_per_dist'] = np.load(
+        os.path.join(simout, 'disp_per_dist.npy'))
+    for a, b, rr in SIM_EVALS:
+        hs.evaluate('ES', os.path.join(simdir, 'labels_<chrom>.txt'),
+                    min_dist=a, max_dist=b, rerun_bh=rr)
+        fn = 'eval.npz' if a is None and b is None else 'eval_%s_%s.npz' % (a, b)
+        e = np.load(os.path.join(simout, fn))
+        for k in ('fdr', 'fpr', 'tpr', 'thresh'):
+            out['eval__%s__%s' % (fn[:-4], k)] = e[k]
+    np.savez_compressed(os.path.join(HERE, 'sim_%s.npz' % name), **out)
+    print('sim', name, {c: np.unique(out['labels__%s' % c], return_counts=True)
+                        for c in chroms})
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['e2e', 'special', 'nb', 'lowess', 'scaling',
                              'calls', 'clusters', 'alt', 'norms', 'lwdrop',
-                             'hard_cfg2']
+                             'hard_cfg2', 'sim']
     for w in which:
         if w.startswith('e2e:'):
             run_e2e(w[4:])
@@ -605,6 +695,8 @@ if __name__ == '__main__':
         run_lowess_drop()
     if 'hard_cfg2' in which:
         run_hard_cfg2()
+    if 'sim' in which:
+        run_sim()
     if 'alt' in which:
         run_alternatives('small2')
     if 'calls' in which:
