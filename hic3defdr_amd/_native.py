@@ -28,7 +28,7 @@ EXPORTS = [
     'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
-    'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel',
+    'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
 ]
 
 
@@ -102,6 +102,9 @@ def load_library(path=None):
                                          _P, _P, _P]),
             'h3d_mme_per_pixel': (_I, [_P, _P, _P, _I64, _I, _I, _P, _D,
                                        _P]),
+            'h3d_lrt_wide': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I, _P,
+                                  _P, _P, _P]),
+            'h3d_cml': (_I, [_P, _P, _I64, _I, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -277,6 +280,32 @@ class Context(object):
             _ptr(cond), D, int(bool(refit_mu)), _ptr(p), _ptr(llr), _ptr(mu0),
             _ptr(mu1), _ptr(disp)), 'h3d_lrt')
         return p, llr, mu0, mu1, disp
+
+    def lrt_wide(self, raw, f, disp_wide, cond_of_rep, C, refit_mu=True):
+        """lrt.py's own call: per pixel and replicate dispersions (n, R)."""
+        raw = _c(raw, np.int64)
+        f = _c(f, np.float64)
+        dw = _c(disp_wide, np.float64)
+        cond = _c(cond_of_rep, np.int32)
+        n, R = raw.shape
+        if f.shape != (n, R) or dw.shape != (n, R):
+            raise ValueError('raw, f and disp must all be (n, R)')
+        p, llr, mu0 = np.empty(n), np.empty(n), np.empty(n)
+        mu1 = np.empty((n, C))
+        _check(self.lib.h3d_lrt_wide(
+            self.handle, _ptr(raw), _ptr(f), _ptr(dw), n, R, C, _ptr(cond),
+            int(bool(refit_mu)), _ptr(p), _ptr(llr), _ptr(mu0), _ptr(mu1)),
+            'h3d_lrt_wide')
+        return p, llr, mu0, mu1
+
+    def cml(self, data):
+        """cml on (n, r) data already divided by f."""
+        data = _c(data, np.float64)
+        n, r = data.shape
+        out = ctypes.c_double(0)
+        _check(self.lib.h3d_cml(self.handle, _ptr(data), n, r,
+                                ctypes.byref(out)), 'h3d_cml')
+        return out.value
 
     def lrt_dev(self, d_raw, d_f, d_dist, disp_table, n, R, cond_of_rep,
                 d_p, d_llr, d_mu0, d_mu1, d_disp=None, refit_mu=True):

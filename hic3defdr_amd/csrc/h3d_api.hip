@@ -189,10 +189,10 @@ void launch_lrt(h3d_ctx* ctx, int grid, const int32_t* raw, const double* f,
                 const int32_t* dist, const double* table, int64_t n, int R,
                 int C, int D, const int32_t* cond, int refit, double* p,
                 double* llr, double* mu0, double* mu1, double* disp,
-                int* flags) {
+                int* flags, int wide) {
   hipLaunchKernelGGL((k_lrt<M, CM>), dim3(grid), dim3(kBlock), 0, ctx->stream,
                      raw, f, dist, table, n, R, C, D, cond, refit, p, llr, mu0,
-                     mu1, disp, flags);
+                     mu1, disp, flags, wide);
 }
 
 int flags_to_code(int fl) {
@@ -657,12 +657,18 @@ int h3d_disp_table(const double* col, int D, int weighted, double frac,
 // lrt
 // ---------------------------------------------------------------------------
 
-int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
-                const int32_t* d_dist, const double* disp_table, int64_t n,
-                int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
-                double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
-                double* d_disp) {
+}  // extern "C"
+
+namespace {
+
+// wide: disp_table is per pixel AND replicate (n, R) (d_dist must be null)
+int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+            const int32_t* d_dist, const double* disp_table, int64_t n, int R,
+            int C, const int32_t* cond_of_rep, int D, int refit_mu, double* d_p,
+            double* d_llr, double* d_mu0, double* d_mu1, double* d_disp,
+            int wide) {
   if (!ctx || !disp_table || !cond_of_rep) return fail(H3D_EARG, "null argument");
+  if (wide && (d_dist || d_disp)) return fail(H3D_EARG, "wide dispersions take no dist / disp_out");
   if (n == 0) return 0;
   if (!d_raw || !d_f || !d_p || !d_llr || !d_mu0 || !d_mu1)
     return fail(H3D_EARG, "null device buffer");
@@ -671,8 +677,9 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   if (int rc = check_cond(cond_of_rep, R, C, &nrep, &rep_idx)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  // d_dist == NULL: disp_table holds per-pixel dispersions (n, C)
-  const size_t tab_n = d_dist ? (size_t)D * C : (size_t)n * C;
+  // d_dist == NULL: disp_table holds per-pixel dispersions (n, C), or with
+  // `wide` per pixel and replicate (n, R)
+  const size_t tab_n = d_dist ? (size_t)D * C : (size_t)n * (wide ? R : C);
   double* d_tab = (double*)scratch(ctx, "disp_table", tab_n * 8);
   int32_t* d_cond = (int32_t*)scratch(ctx, "cond_of_rep", R * 4);
   int* d_fl = (int*)scratch(ctx, "lrt_flags", 4);
@@ -687,7 +694,7 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     const int cm = C <= 2 ? 2 : C <= 4 ? 4 : 8;
 #define H3D_LRT(MM, CC)                                                          \
   launch_lrt<MM, CC>(ctx, grid, d_raw, d_f, d_dist, d_tab, n, R, C, D, d_cond,   \
-                     refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, d_fl)
+                     refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, d_fl, wide)
     if (m == 4 && cm == 2) H3D_LRT(4, 2);
     else if (m == 4 && cm == 4) H3D_LRT(4, 4);
     else if (m == 8 && cm == 2) H3D_LRT(8, 2);
@@ -705,10 +712,11 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   return flags_to_code(fl);
 }
 
-int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
-            const int32_t* dist, const double* disp_table, int64_t n, int R,
-            int C, const int32_t* cond_of_rep, int D, int refit_mu, double* p,
-            double* llr, double* mu0, double* mu1, double* disp_out) {
+// host buffers in and out (h3d_lrt / h3d_lrt_wide)
+int lrt_host(h3d_ctx* ctx, const int64_t* raw, const double* f, const int32_t* dist,
+             const double* disp_table, int64_t n, int R, int C,
+             const int32_t* cond_of_rep, int D, int refit_mu, double* p, double* llr,
+             double* mu0, double* mu1, double* disp_out, int wide) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   if (n == 0) return 0;
   if (!raw || !f || !p || !llr || !mu0 || !mu1) return fail(H3D_EARG, "null buffer");
@@ -730,8 +738,8 @@ int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
                      d_raw64, d_raw, n * R, d_ovf);
   double *dp = d_out, *dl = d_out + n, *dm0 = d_out + 2 * n, *dm1 = d_out + 3 * n,
          *dd = d_out + (3 + C) * n;
-  int rc = h3d_lrt_dev(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep,
-                       D, refit_mu, dp, dl, dm0, dm1, disp_out ? dd : nullptr);
+  int rc = lrt_run(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep, D,
+                   refit_mu, dp, dl, dm0, dm1, disp_out ? dd : nullptr, wide);
   int ovf = 0;
   HIP_TRY(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(p, dp, n * 8, hipMemcpyDeviceToHost, s));
@@ -742,6 +750,86 @@ int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
   HIP_TRY(hipStreamSynchronize(s));
   if (ovf) return fail(H3D_EINPUT, "raw counts must be in [0, 2^31)");
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                const int32_t* d_dist, const double* disp_table, int64_t n,
+                int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
+                double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
+                double* d_disp) {
+  return lrt_run(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep, D, refit_mu,
+                 d_p, d_llr, d_mu0, d_mu1, d_disp, 0);
+}
+
+int h3d_lrt_wide(h3d_ctx* ctx, const int64_t* raw, const double* f,
+                 const double* disp_wide, int64_t n, int R, int C,
+                 const int32_t* cond_of_rep, int refit_mu, double* p, double* llr,
+                 double* mu0, double* mu1) {
+  return lrt_host(ctx, raw, f, nullptr, disp_wide, n, R, C, cond_of_rep, 0, refit_mu, p,
+                  llr, mu0, mu1, nullptr, 1);
+}
+
+int h3d_lrt(h3d_ctx* ctx, const int64_t* raw, const double* f,
+            const int32_t* dist, const double* disp_table, int64_t n, int R,
+            int C, const int32_t* cond_of_rep, int D, int refit_mu, double* p,
+            double* llr, double* mu0, double* mu1, double* disp_out) {
+  return lrt_host(ctx, raw, f, dist, disp_table, n, R, C, cond_of_rep, D, refit_mu, p,
+                  llr, mu0, mu1, disp_out, 0);
+}
+
+// ---------------------------------------------------------------------------
+// cml on given data (util/dispersion.py:46-80)
+// ---------------------------------------------------------------------------
+
+int h3d_cml(h3d_ctx* ctx, const double* data, int64_t n, int r, double* disp_out) {
+  if (!ctx || !data || !disp_out) return fail(H3D_EARG, "null argument");
+  if (n < 1 || r < 1 || r > kMaxReps) return fail(H3D_EARG, "n=%lld r=%d", (long long)n, r);
+  if (n >= (int64_t)1 << 31) return fail(H3D_EARG, "n too large");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  // replicate-major (SoA) copy of the data: the pseudodata layout k_brent reads
+  std::vector<double> soa((size_t)n * r);
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = 0; k < r; ++k) soa[(size_t)k * n + i] = data[i * r + k];
+  SegState st;
+  seg_init(&st, n, r);  // phase kEqualize: the first evaluation is at x0
+  std::vector<int32_t> rep_idx(kMaxReps);
+  for (int k = 0; k < kMaxReps; ++k) rep_idx[k] = k;
+  const int64_t seg[2] = {0, n};
+  const int32_t nrep = r;
+  double* d_pd = (double*)scratch(ctx, "cml_pd", (size_t)n * r * 8);
+  int64_t* d_seg = (int64_t*)scratch(ctx, "cml_seg", 16);
+  int32_t* d_ri = (int32_t*)scratch(ctx, "cml_ri", kMaxReps * 4);
+  int32_t* d_nr = (int32_t*)scratch(ctx, "cml_nr", 4);
+  SegState* d_st = (SegState*)scratch(ctx, "cml_st", sizeof(SegState));
+  int* d_fl = (int*)scratch(ctx, "cml_fl", 4);
+  double* d_res = (double*)scratch(ctx, "cml_res", 8);
+  int* d_q = (int*)scratch(ctx, "cml_queue", 4);
+  if (!d_pd || !d_seg || !d_ri || !d_nr || !d_st || !d_fl || !d_res || !d_q)
+    return fail(H3D_ENOMEM, "cml scratch");
+  HIP_TRY(hipMemcpyAsync(d_pd, soa.data(), soa.size() * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_seg, seg, 16, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_ri, rep_idx.data(), kMaxReps * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_nr, &nrep, 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_st, &st, sizeof(SegState), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
+  const int m = r <= 4 ? 4 : r <= 8 ? 8 : r <= 16 ? 16 : 32;
+  if (m == 4) launch_brent<4>(ctx, d_pd, n, d_seg, 1, 1, d_ri, d_nr, d_st, d_fl, d_res, d_q);
+  else if (m == 8) launch_brent<8>(ctx, d_pd, n, d_seg, 1, 1, d_ri, d_nr, d_st, d_fl, d_res, d_q);
+  else if (m == 16) launch_brent<16>(ctx, d_pd, n, d_seg, 1, 1, d_ri, d_nr, d_st, d_fl, d_res, d_q);
+  else launch_brent<32>(ctx, d_pd, n, d_seg, 1, 1, d_ri, d_nr, d_st, d_fl, d_res, d_q);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(&st, d_st, sizeof(SegState), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (st.flags & kFlagBrentFail)
+    return fail(H3D_ENOCONV, "bounded minimisation failed (reference: assert res.success)");
+  // the search ended in seg_step's qcml update: disp = delta / (1 - delta)
+  *disp_out = st.disp;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -593,20 +593,21 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
     int64_t n, int R, int C, int D, const int32_t* __restrict__ cond_of_rep,
     int refit, double* __restrict__ p, double* __restrict__ llr,
     double* __restrict__ mu0, double* __restrict__ mu1,
-    double* __restrict__ disp_out, int* __restrict__ flags) {
+    double* __restrict__ disp_out, int* __restrict__ flags, int wide) {
   int cond[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) cond[k] = (k < R) ? cond_of_rep[k] : -1;
   int fl_all = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    // dist == nullptr: `table` holds per-pixel dispersions (n, C)
+    // dist == nullptr: `table` holds per-pixel dispersions, (n, C) -- or,
+    // with `wide`, per replicate (n, R): lrt.py's disp argument as given
     const int d = dist ? dist[i] : 0;
-    const double* trow = dist ? table + (int64_t)d * C : table + i * C;
+    const double* trow = dist ? table + (int64_t)d * C : table + i * (wide ? R : C);
     const bool inb = dist ? (d >= 0 && d < D) : true;
     double dc[CM];
 #pragma unroll
-    for (int c = 0; c < CM; ++c) dc[c] = (c < C && inb) ? trow[c] : NAN;
+    for (int c = 0; c < CM; ++c) dc[c] = (c < C && inb && !wide) ? trow[c] : NAN;
     double x[M], fv[M], a[M];
 #pragma unroll
     for (int k = 0; k < M; ++k) {
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
 #pragma unroll
         for (int c = 0; c < CM; ++c)
           if (c == cond[k]) ak = dc[c];
-        a[k] = ak;
+        a[k] = wide ? trow[k] : ak;
       } else {
         x[k] = 0.0;
         fv[k] = 1.0;

@@ -1,0 +1,59 @@
+"""Operator-level drop-ins for the reference's dispersion estimators
+(hic3defdr/util/dispersion.py): same signatures; computed on the GPU.
+
+- ``qcml(data, f)``: one (distance, condition) segment through the
+  estimate_disp device driver (equalize + bounded Brent, k_disp_work /
+  k_brent) -- the estimator ``estimate_disp(estimator='qcml')`` calls;
+- ``cml(data, f)``: one bounded-Brent search (h3d_cml);
+- ``mme_per_pixel`` / ``mme``: the per-pixel method-of-moments kernel.
+
+As in the reference, ``cml`` / ``mme`` / ``mme_per_pixel`` divide ``data``
+by ``f`` IN PLACE (dispersion.py:67-68, 101-102, 129-130): float data is
+modified, integer data raises numpy's casting error (which is why the
+reference's estimate_disp cannot use them on raw counts)."""
+import numpy as np
+
+from hic3defdr_amd import _native
+
+
+def qcml(data, f=None, max_iter=10, tol=1e-4):
+    """dispersion.py:10-43. ``max_iter`` is accepted and, as in the
+    reference (whose loop counter is never incremented), has no effect; the
+    convergence tolerance is the reference's default 1e-4."""
+    data = np.asarray(data)
+    if tol != 1e-4:
+        raise NotImplementedError('the device qcml converges at tol=1e-4')
+    if data.ndim != 2:
+        raise ValueError('data must be (pixels, replicates)')
+    if data.size and not np.all(data == np.floor(data)):
+        raise ValueError('qcml takes integer counts')
+    n, r = data.shape
+    f = np.ones((n, r)) if f is None else np.broadcast_to(f, (n, r))
+    ctx = _native.context()
+    out = ctx.disp_per_dist(data.astype(np.int64), f, np.zeros(n, np.int32),
+                            np.zeros(r, np.int32), 1, 1)
+    return float(out[0, 0])
+
+
+def cml(data, f=None):
+    """dispersion.py:46-80."""
+    if f is not None:
+        data /= f   # in place, as the reference
+    return _native.context().cml(np.asarray(data, dtype=np.float64))
+
+
+def mme_per_pixel(data, f=None):
+    """dispersion.py:83-105."""
+    if f is not None:
+        data /= f
+    data = np.asarray(data, dtype=np.float64)
+    ctx = _native.context()
+    return ctx.mme_per_pixel(data, None, np.zeros(data.shape[1], np.int32),
+                             1)[:, 0]
+
+
+def mme(data, f=None):
+    """dispersion.py:108-131."""
+    if f is not None:
+        data /= f
+    return np.nanmean(mme_per_pixel(data))

@@ -16,6 +16,8 @@
  *                              util/lowess.py:10-244 (the fitted disp_fn,
  *                              tabulated on every integer distance)
  *   h3d_lrt                <- util/lrt.py:7-50 (+ analysis/analysis.py:272-278)
+ *   h3d_lrt_wide           <- util/lrt.py:7 lrt(raw, f, disp, design) as called
+ *   h3d_cml                <- util/dispersion.py:46-80 cml
  *   h3d_bh                 <- analysis/analysis.py:286-303 (lib5c
  *                              adjust_pvalues = BH)
  *   h3d_find_clusters      <- util/clusters.py:73-97 find_clusters (threshold /
@@ -159,6 +161,21 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                 int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
                 double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
                 double* d_disp);
+
+/* lrt.py:7-50 with the reference's own disp argument: per pixel AND
+ * replicate dispersions disp_wide (n, R) (lrt.py's `disp`, as analysis.py:277
+ * builds it with np.dot(disp, design.T); any (n, R) values are taken as
+ * given). Outputs as h3d_lrt. */
+int h3d_lrt_wide(h3d_ctx* ctx, const int64_t* raw, const double* f,
+                 const double* disp_wide, int64_t n, int R, int C,
+                 const int32_t* cond_of_rep, int refit_mu, double* p,
+                 double* llr, double* mu0, double* mu1);
+
+/* dispersion.py:46-80 cml on given data (n, r), already divided by f: the
+ * bounded-Brent minimisation of the NB conditional NLL on the GPU (one
+ * k_brent search); *disp = delta / (1 - delta). H3D_ENOCONV where the
+ * reference's assert res.success would fail. */
+int h3d_cml(h3d_ctx* ctx, const double* data, int64_t n, int r, double* disp);
 
 /* ---- bh ---------------------------------------------------------------- */
 

@@ -1,0 +1,148 @@
+"""The hot path at the other north-star shapes (BASELINE.json configs /
+SURVEY.md §8(d)) on one GPU, the way bench.py times cfg2: estimate_disp
+(qcml per distance x condition + lowess table) + lrt on HBM-resident
+inputs.
+
+    cfg3: mouse genome at 10 kb -- 20 chromosomes, ~265k bins, R = 4 (2 + 2),
+          dist_thresh_max 200, one genome-wide pooled estimate_disp
+    cfg4: human chr1 at 5 kb -- 49,792 bins, R = 18 (6 + 6 + 6), C = 3,
+          dist_thresh_max 400 (chi2 df = 2, k_lrt<32, 8>, the M = 8 disp path)
+
+The pixels are drawn directly in the band (no files; the SURVEY §8(d)
+generator's model: mu(d) = 400 (d+1)^-1, 0.2 % loops x5, 1 % differential
+x2 in conditions >= 1, per-bin bias exp(N(0, .25)), depth 0.8 + 0.1 k,
+NB(1/0.05)); disp_idx = every condition's mean of raw / (b_i b_j) >= 1 and
+d >= 4, as prepare_data with unit size factors. Prints one JSON line.
+
+    python tools/run_cfg.py --cfg 3 [--steps 3 --warmup 1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+MM10 = [19535, 18211, 16007, 15649, 15171, 14950, 14546, 12930, 12459, 13069,
+        12208, 12013, 12042, 12490, 10404, 9820, 9499, 9070, 6143, 17102]
+CFGS = {
+    3: dict(chroms=MM10, npc=(2, 2), dmax=200),
+    4: dict(chroms=[49792], npc=(6, 6, 6), dmax=400),
+}
+
+
+def draw(bins_list, npc, dmax, seed=0):
+    rng = np.random.default_rng(seed)
+    R = sum(npc)
+    cond = np.repeat(np.arange(len(npc)), npc).astype(np.int32)
+    raws, fs, dists = [], [], []
+    for n_bins in bins_list:
+        d = np.concatenate([np.full(n_bins - k, k, dtype=np.int32)
+                            for k in range(min(dmax, n_bins - 1) + 1)])
+        r = np.concatenate([np.arange(n_bins - k, dtype=np.int32)
+                            for k in range(min(dmax, n_bins - 1) + 1)])
+        c = r + d
+        base = 400.0 / (d + 1.0)
+        base *= np.where(rng.random(d.size) < 0.002, 5.0, 1.0)
+        diff = rng.random(d.size) < 0.01
+        raw = np.empty((d.size, R), dtype=np.int32)
+        f = np.empty((d.size, R))
+        for k in range(R):
+            b = np.exp(rng.normal(0, 0.25, n_bins))
+            bb = b[r] * b[c]
+            mu = base * np.where(diff & (cond[k] >= 1), 2.0, 1.0) * bb * \
+                (0.8 + 0.1 * (k % 4))
+            raw[:, k] = rng.negative_binomial(20.0, 20.0 / (20.0 + mu))
+            f[:, k] = bb
+        keep = d >= 4
+        for ci in range(len(npc)):
+            keep &= (raw[:, cond == ci] / f[:, cond == ci]).mean(axis=1) >= 1.0
+        raws.append(raw[keep])
+        fs.append(f[keep])
+        dists.append(d[keep])
+        print('  chrom of %d bins: %d band px, %d disp px' %
+              (n_bins, d.size, keep.sum()), file=sys.stderr, flush=True)
+    return (np.concatenate(raws), np.concatenate(fs), np.concatenate(dists),
+            cond)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--cfg', type=int, choices=sorted(CFGS), required=True)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    args = ap.parse_args()
+    cfg = CFGS[args.cfg]
+    t0 = time.time()
+    raw, f, dist, cond = draw(cfg['chroms'], cfg['npc'], cfg['dmax'])
+    gen_s = time.time() - t0
+    import torch
+    from hic3defdr_amd import _native
+    torch.cuda.set_device(0)
+    ctx = _native.context(0)
+    dev = torch.device('cuda', 0)
+    n, R = raw.shape
+    C = len(cfg['npc'])
+    D = cfg['dmax'] + 1
+    t_raw = torch.from_numpy(raw).to(dev)
+    t_f = torch.from_numpy(f).to(dev)
+    t_d = torch.from_numpy(dist).to(dev)
+    t_p = torch.empty(n, dtype=torch.float64, device=dev)
+    t_llr, t_m0 = torch.empty_like(t_p), torch.empty_like(t_p)
+    t_m1 = torch.empty((n, C), dtype=torch.float64, device=dev)
+    t_disp = torch.empty_like(t_m1)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+
+    def step():
+        dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                    t_d.data_ptr(), n, R, cond, C, D)
+        tab = _native.disp_tables(dpd)
+        ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), tab, n,
+                    R, cond, t_p.data_ptr(), t_llr.data_ptr(),
+                    t_m0.data_ptr(), t_m1.data_ptr(), t_disp.data_ptr())
+        return dpd
+
+    for _ in range(args.warmup):
+        first = step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dpd = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ctx.profile_reset()
+    ctx.profile(True, level=2)
+    step()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    ks = {k: ctx.profile_read(k)[0] for k in
+          ('disp_work', 'disp_nll', 'disp_update', 'disp_prep', 'lrt')}
+    p = t_p.cpu().numpy()
+    present = np.isin(np.arange(D), dist)
+    out = {
+        'config': 'cfg%d' % args.cfg, 'bins': int(sum(cfg['chroms'])),
+        'chroms': len(cfg['chroms']), 'reps': R, 'conds': C,
+        'dist_thresh_max': cfg['dmax'], 'disp_pixels': int(n),
+        'value': n * args.steps / el, 'unit': 'pixels/s',
+        'ms_per_step': el / args.steps * 1e3, 'steps': args.steps,
+        'kernels_ms_per_step': ks,
+        'checks': {
+            'disp_finite_where_present': bool(np.all(np.isfinite(
+                dpd[present]))),
+            'disp_nan_where_absent': bool(np.all(np.isnan(dpd[~present]))),
+            'p_in_0_1': bool(np.all((p >= 0) & (p <= 1))),
+            'deterministic_disp': bool(np.array_equal(first, dpd)),
+            'frac_p_lt_0.05': float(np.mean(p < 0.05))},
+        'generate_s': gen_s,
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
