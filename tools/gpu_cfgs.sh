@@ -6,14 +6,10 @@ set -e
 tag=${1:-c}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_operators.py tests/test_gpu_simulation.py \
-  -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || \
-  { tail -n 40 gpurun_out/${tag}_tests.log; exit 1; }
 for c in 4 3; do
   timeout -k 10 400 python3 -u tools/run_cfg.py --cfg $c > gpurun_out/${tag}_cfg$c.json 2> gpurun_out/${tag}_cfg$c.err
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
     -d gpurun_out/${tag}_prof_cfg$c -o run -- python3 -u tools/run_cfg.py --cfg $c --steps 1 \
     > gpurun_out/${tag}_prof_cfg$c.json 2> gpurun_out/${tag}_prof_cfg$c.err
 done
-tail -n 3 gpurun_out/${tag}_tests.log
 cat gpurun_out/${tag}_cfg4.json gpurun_out/${tag}_cfg3.json

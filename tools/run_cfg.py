@@ -95,6 +95,7 @@ def main():
     t_llr, t_m0 = torch.empty_like(t_p), torch.empty_like(t_p)
     t_m1 = torch.empty((n, C), dtype=torch.float64, device=dev)
     t_disp = torch.empty_like(t_m1)
+    torch.cuda.synchronize()   # the uploads ran on the default stream
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
@@ -137,7 +138,8 @@ def main():
                 dpd[present]))),
             'disp_nan_where_absent': bool(np.all(np.isnan(dpd[~present]))),
             'p_in_0_1': bool(np.all((p >= 0) & (p <= 1))),
-            'deterministic_disp': bool(np.array_equal(first, dpd)),
+            'deterministic_disp': bool(np.array_equal(first, dpd,
+                                                      equal_nan=True)),
             'frac_p_lt_0.05': float(np.mean(p < 0.05))},
         'generate_s': gen_s,
     }
