@@ -17,6 +17,7 @@ and header it is built from, and is rebuilt whenever that digest changes. A
 binary copied from another tree (or a stale one whose sources were edited
 with an older mtime) is therefore never silently reused.
 """
+import concurrent.futures
 import hashlib
 import os
 import subprocess
@@ -31,11 +32,14 @@ HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 
 # (source, compiler): device TUs through hipcc, host-only TUs through g++
-NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
+NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_lrt.hip', 'hipcc'),
+               ('h3d_prepare_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
                ('h3d_calls.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
-           'h3d_prepare.h', 'h3d_prepare_api.h', 'h3d_errors.h',
-           'h3d_ctx.h', 'h3d_norms.h']
+           'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h']
+# concurrent compiles (each hipcc TU is single-threaded; the box sets
+# MAX_JOBS=16, this container has 8 CPUs)
+JOBS = max(1, min(int(os.environ.get('MAX_JOBS', '8')), os.cpu_count() or 1))
 HIP_FLAGS = ['--offload-arch=%s' % ARCH, '-O3', '-std=c++17', '-fPIC',
              '-munsafe-fp-atomics']
 
@@ -94,30 +98,54 @@ def build_selftest(force=False):
     return _build(out, cmd, [src] + _headers(), force)
 
 
-def build_native(force=False):
-    """Compiles each TU to an object, then links libh3d.so with hipcc; each
-    step is skipped when its content digest is unchanged."""
-    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
-    out = os.path.join(LIBDIR, 'libh3d.so')
+def _native_objects():
+    """(object, compile command, deps) of every TU of libh3d.so."""
     hdrs = _headers()
-    objs = []
+    jobs = []
     for src, cc in NATIVE_SRCS:
         s = os.path.join(CSRC, src)
         o = os.path.join(LIBDIR, 'obj', src + '.o')
-        objs.append(o)
         if cc == 'hipcc':
             cmd = [HIPCC] + HIP_FLAGS + ['-I', INC, '-c', '-o', o, s]
         else:
             cmd = ['g++', '-O2', '-std=c++17', '-fPIC', '-I', INC, '-c', '-o',
                    o, s]
-        _build(o, cmd, [s] + hdrs, force)
+        jobs.append((o, cmd, [s] + hdrs))
+    return jobs
+
+
+def _link_native(force):
+    out = os.path.join(LIBDIR, 'libh3d.so')
+    objs = [o for o, _, _ in _native_objects()]
     cmd = [HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out] \
         + objs
     return _build(out, cmd, objs, force)
 
 
+def build_native(force=False):
+    """Compiles each TU to an object (concurrently), then links libh3d.so
+    with hipcc; each step is skipped when its content digest is unchanged."""
+    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
+    with concurrent.futures.ThreadPoolExecutor(JOBS) as ex:
+        for f in [ex.submit(_build, o, c, d, force)
+                  for o, c, d in _native_objects()]:
+            f.result()
+    return _link_native(force)
+
+
 def build_all(force=False):
-    return build_native(force), build_hosttest(force), build_selftest(force)
+    """libh3d.so, libh3d_hosttest.so and libh3d_selftest.so; every compile
+    step of the three runs concurrently."""
+    os.makedirs(os.path.join(LIBDIR, 'obj'), exist_ok=True)
+    with concurrent.futures.ThreadPoolExecutor(JOBS) as ex:
+        futs = [ex.submit(_build, o, c, d, force)
+                for o, c, d in _native_objects()]
+        futs += [ex.submit(build_hosttest, force),
+                 ex.submit(build_selftest, force)]
+        for f in futs:
+            f.result()
+    return (_link_native(force), os.path.join(LIBDIR, 'libh3d_hosttest.so'),
+            os.path.join(LIBDIR, 'libh3d_selftest.so'))
 
 
 if __name__ == '__main__':

@@ -81,6 +81,8 @@ struct h3d_ctx {
                    // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
   int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
   int nll_w = 1;  // H3D_NLL_W: min waves/SIMD of the NLL-only pass (1, 2, 4)
+  int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
+                    // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)
 };
 
 namespace h3dint {
@@ -98,6 +100,8 @@ int grid_for(h3d_ctx* ctx, int64_t n, int per_cu = 8);
 // replicate indices (C x kMaxReps, design order)
 int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
                std::vector<int32_t>* rep_idx);
+// kernel status flags -> H3D_E* code (+ message)
+int flags_to_code(int fl);
 
 // wraps one kernel launch with HIP events on the ctx stream when profiling
 struct ProfScope {

@@ -48,7 +48,7 @@ __device__ inline double block_sum(double v, double* lds) {
   return t;
 }
 
-__global__ void k_i64_to_i32(const int64_t* __restrict__ in,
+static __global__ void k_i64_to_i32(const int64_t* __restrict__ in,
                              int32_t* __restrict__ out, int64_t n,
                              int* __restrict__ overflow) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -59,14 +59,14 @@ __global__ void k_i64_to_i32(const int64_t* __restrict__ in,
   }
 }
 
-__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
+static __global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (int32_t)i;
 }
 
 // AoS (n, R) -> distance-sorted SoA [r][i]
-__global__ void k_gather_soa(const int32_t* __restrict__ perm,
+static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
                              const int32_t* __restrict__ raw,
                              const double* __restrict__ f, int64_t n, int R,
                              int32_t* __restrict__ raw_s,
@@ -138,7 +138,7 @@ __global__ void k_key_dist(const K* __restrict__ keys, int64_t n, int cbits,
 }
 
 // seg_start[d] = first index with dist_s >= d (d = 0..D)
-__global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
+static __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t n,
                              int D, int64_t* __restrict__ seg_start) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d > D) return;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
 // wave then advances its segment's qcml/Brent state machine itself: the
 // segments step in parallel across the chip instead of inside the single
 // list-building workgroup of k_seg_update.
-__global__ void k_seg_reduce(const double* __restrict__ partial,
+static __global__ void k_seg_reduce(const double* __restrict__ partial,
                              const int32_t* __restrict__ seg_lb,
                              const int32_t* __restrict__ seg_le, int S,
                              double* __restrict__ seg_total,
@@ -350,7 +350,7 @@ __global__ void k_seg_reduce(const double* __restrict__ partial,
 // One workgroup: with `step`, advance every active segment's qcml/Brent
 // state machine with its (rank-reduced) total -- otherwise k_seg_reduce has
 // already stepped them -- then rebuild the active work list.
-__global__ __launch_bounds__(1024) void k_seg_update(
+static __global__ __launch_bounds__(1024) void k_seg_update(
     SegState* __restrict__ st, const double* __restrict__ seg_total,
     const int* __restrict__ seg_flags, int S, int C,
     const int32_t* __restrict__ n_rep, const int32_t* __restrict__ seg_chunk_b,
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(1024) void k_seg_update(
 // more than the tail the static grid leaves idle.
 // seg_step out of line for k_brent: run by one thread once per evaluation,
 // its registers stay out of the NLL loop's budget
-__device__ __noinline__ void seg_step_ool(SegState* s, double total, int n_reps) {
+static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int n_reps) {
   seg_step(s, total, n_reps);
 }
 
@@ -546,20 +546,23 @@ __global__ __launch_bounds__(kBrentBlock, 4) void k_brent(
     while (true) {
       const NllConst kc = s_st.k;
       double acc = 0.0;
-      // next pixel's pseudodata loaded one iteration ahead (latency hidden
-      // behind the current pixel's lgammas)
-      int64_t px = b + threadIdx.x;
-      double v[M];
+      // two pixels per iteration (px, px + block): their lgammas are
+      // independent chains the scheduler interleaves (the NLL is bound by
+      // FP64 dependency latency at 4 waves/SIMD); the terms still join the
+      // sum in pixel order
+      for (int64_t px = b + threadIdx.x; px < e; px += 2 * kBrentBlock) {
+        const int64_t qx = px + kBrentBlock;
+        const bool two = qx < e;
+        double v[M], w[M];
 #pragma unroll
-      for (int k = 0; k < M; ++k) v[k] = (k < nr && px < e) ? pd[(int64_t)ri[k] * n + px] : 0.0;
-      for (; px < e; px += kBrentBlock) {
-        const int64_t nx = px + kBrentBlock;
-        double w[M];
-#pragma unroll
-        for (int k = 0; k < M; ++k) w[k] = (k < nr && nx < e) ? pd[(int64_t)ri[k] * n + nx] : 0.0;
-        acc += nll_pixel<M>(v, nr, kc);
-#pragma unroll
-        for (int k = 0; k < M; ++k) v[k] = w[k];
+        for (int k = 0; k < M; ++k) {
+          v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
+          w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
+        }
+        const double t0 = nll_pixel<M>(v, nr, kc);
+        const double t1 = nll_pixel<M>(w, nr, kc);
+        acc += t0;
+        if (two) acc += t1;
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);

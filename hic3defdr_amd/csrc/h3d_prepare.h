@@ -23,14 +23,14 @@ namespace h3d {
 // (the union state PrepUnion lives in h3d_ctx.h, inside the h3d_ctx)
 
 // row id of every CSR entry (one thread per row)
-__global__ void k_csr_rows(const int64_t* __restrict__ indptr, int n_bins,
+static __global__ void k_csr_rows(const int64_t* __restrict__ indptr, int n_bins,
                            int32_t* __restrict__ row_of) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_bins) return;
   for (int64_t j = indptr[i]; j < indptr[i + 1]; ++j) row_of[j] = i;
 }
 
-__global__ void k_union_keys(const int32_t* __restrict__ row_of,
+static __global__ void k_union_keys(const int32_t* __restrict__ row_of,
                              const int32_t* __restrict__ col,
                              const double* __restrict__ val, int64_t n_ent,
                              int64_t ent_offset, int rep, int R, int n_bins,
@@ -56,7 +56,7 @@ __global__ void k_union_keys(const int32_t* __restrict__ row_of,
 }
 
 // head[i] = 1 where a new non-sentinel key starts
-__global__ void k_run_heads(const int64_t* __restrict__ keys, int64_t n,
+static __global__ void k_run_heads(const int64_t* __restrict__ keys, int64_t n,
                             int64_t sentinel, int32_t* __restrict__ head) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -66,7 +66,7 @@ __global__ void k_run_heads(const int64_t* __restrict__ keys, int64_t n,
 }
 
 // run starts: run r begins at the entry whose inclusive head-scan equals r+1
-__global__ void k_run_starts(const int32_t* __restrict__ head,
+static __global__ void k_run_starts(const int32_t* __restrict__ head,
                              const int32_t* __restrict__ run_incl, int64_t n,
                              int64_t* __restrict__ run_start) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -75,7 +75,7 @@ __global__ void k_run_starts(const int32_t* __restrict__ head,
 }
 
 // keep flag per run: deconvoluted sum finite and > 0
-__global__ void k_run_keep(const int64_t* __restrict__ keys,
+static __global__ void k_run_keep(const int64_t* __restrict__ keys,
                            const int32_t* __restrict__ ent_sorted,
                            const int64_t* __restrict__ run_start,
                            int64_t n_runs, int64_t n_ent, int64_t sentinel,
@@ -100,7 +100,7 @@ __global__ void k_run_keep(const int64_t* __restrict__ keys,
 }
 
 // fill row/col/raw/balanced for kept runs (px = exclusive scan of keep)
-__global__ void k_union_fill(const int64_t* __restrict__ keys,
+static __global__ void k_union_fill(const int64_t* __restrict__ keys,
                              const int32_t* __restrict__ ent_sorted,
                              const int64_t* __restrict__ run_start,
                              const int32_t* __restrict__ keep,
@@ -140,7 +140,7 @@ __global__ void k_union_fill(const int64_t* __restrict__ keys,
 // equal_bin with the stable tie order: sorted position k -> bin
 // floor(k * (n_bins / n)) (numpy linspace(0, n_bins, n, endpoint=False,
 // dtype=int)); bin_of_sorted[k]
-__global__ void k_equal_bin(int64_t n, int n_bins, int32_t* __restrict__ bin) {
+static __global__ void k_equal_bin(int64_t n, int n_bins, int32_t* __restrict__ bin) {
   const double step = (double)n_bins / (double)n;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
        k += (int64_t)gridDim.x * blockDim.x)
@@ -149,7 +149,7 @@ __global__ void k_equal_bin(int64_t n, int n_bins, int32_t* __restrict__ bin) {
 
 // bin boundaries over the sorted positions: bin_start[b] = first k with
 // bin[k] >= b (b = 0..n_bins)
-__global__ void k_bin_bounds(const int32_t* __restrict__ bin, int64_t n,
+static __global__ void k_bin_bounds(const int32_t* __restrict__ bin, int64_t n,
                              int n_bins, int64_t* __restrict__ bin_start) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b > n_bins) return;
@@ -167,7 +167,7 @@ __global__ void k_bin_bounds(const int32_t* __restrict__ bin, int64_t n,
 // ratio keys for the median: for sorted position k of bin b, replicate r:
 // data / gmean(data, pseudocount 1) when every replicate > 0 (scaling.py:44-47)
 // else +inf (sorts past the valid ones); valid rows counted per bin.
-__global__ void k_mor_keys(const double* __restrict__ balanced,
+static __global__ void k_mor_keys(const double* __restrict__ balanced,
                            const int32_t* __restrict__ perm, int64_t n, int R,
                            const int32_t* __restrict__ bin,
                            double* __restrict__ keys,
@@ -203,7 +203,7 @@ __global__ void k_mor_keys(const double* __restrict__ balanced,
 
 // per (replicate, bin): median of the first `valid` sorted ratios; d_per_bin
 // = mean distance of the bin (exact: integer sum)
-__global__ void k_mor_median(const double* __restrict__ sorted_keys,
+static __global__ void k_mor_median(const double* __restrict__ sorted_keys,
                              const int64_t* __restrict__ bin_start,
                              const int32_t* __restrict__ valid, int n_bins,
                              int64_t n, int R, double* __restrict__ s_per_bin) {
@@ -222,7 +222,7 @@ __global__ void k_mor_median(const double* __restrict__ sorted_keys,
   s_per_bin[(int64_t)b * R + r] = med;
 }
 
-__global__ void k_bin_dist_sum(const int32_t* __restrict__ dist_sorted,
+static __global__ void k_bin_dist_sum(const int32_t* __restrict__ dist_sorted,
                                const int64_t* __restrict__ bin_start,
                                int n_bins, double* __restrict__ d_per_bin) {
   // one workgroup per bin; integer sum, so the reduction order is free
@@ -245,7 +245,7 @@ __global__ void k_bin_dist_sum(const int32_t* __restrict__ dist_sorted,
 
 // sf[i, r] = interp1d(d_per_bin, s_per_bin[:, r], extrapolate)(dist[i]) over
 // the non-empty bins (compacted by the host: m points)
-__global__ void k_sf_interp(const int32_t* __restrict__ dist, int64_t n, int R,
+static __global__ void k_sf_interp(const int32_t* __restrict__ dist, int64_t n, int R,
                             const double* __restrict__ xp,
                             const double* __restrict__ yp /* m x R */, int m,
                             double* __restrict__ sf) {
@@ -270,7 +270,7 @@ __global__ void k_sf_interp(const int32_t* __restrict__ dist, int64_t n, int R,
 }
 
 // exact-distance mode: sf[i, r] = s_per_bin[bin(dist[i]), r]
-__global__ void k_sf_exact(const int32_t* __restrict__ perm,
+static __global__ void k_sf_exact(const int32_t* __restrict__ perm,
                            const int32_t* __restrict__ bin, int64_t n, int R,
                            const double* __restrict__ s_per_bin,
                            double* __restrict__ sf) {
@@ -283,7 +283,7 @@ __global__ void k_sf_exact(const int32_t* __restrict__ perm,
 
 // bin of every pixel in its original position (bin_of_sorted scattered
 // through the distance sort's permutation)
-__global__ void k_scatter_bin(const int32_t* __restrict__ perm,
+static __global__ void k_scatter_bin(const int32_t* __restrict__ perm,
                               const int32_t* __restrict__ bin_of_sorted,
                               int64_t n, int32_t* __restrict__ bin_orig) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
@@ -295,7 +295,7 @@ __global__ void k_scatter_bin(const int32_t* __restrict__ perm,
 // np.sum(data, axis=0) over the bin's rows in their original order, which
 // numpy accumulates row by row): one lane per (bin, replicate) walks the
 // bin's members (grouped by bin, original order inside) sequentially
-__global__ void k_bin_colsum(const double* __restrict__ balanced,
+static __global__ void k_bin_colsum(const double* __restrict__ balanced,
                              const int32_t* __restrict__ members,
                              const int64_t* __restrict__ bin_start, int n_bins,
                              int R, double* __restrict__ colsum) {
@@ -319,14 +319,14 @@ __global__ void k_bin_colsum(const double* __restrict__ balanced,
 
 // exact mode bins: bin of sorted position = its distance rank among distinct
 // distances (head flags scanned on device)
-__global__ void k_dist_heads(const int32_t* __restrict__ dist_sorted, int64_t n,
+static __global__ void k_dist_heads(const int32_t* __restrict__ dist_sorted, int64_t n,
                              int32_t* __restrict__ head) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
        k += (int64_t)gridDim.x * blockDim.x)
     head[k] = (k == 0 || dist_sorted[k] != dist_sorted[k - 1]) ? 1 : 0;
 }
 
-__global__ void k_minus_one(int32_t* __restrict__ v, int64_t n) {
+static __global__ void k_minus_one(int32_t* __restrict__ v, int64_t n) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
        k += (int64_t)gridDim.x * blockDim.x)
     v[k] -= 1;

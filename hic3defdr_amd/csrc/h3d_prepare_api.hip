@@ -1,6 +1,22 @@
-// prepare_data entry points of libh3d.so (included at the end of
-// h3d_api.hip; shares its ctx / scratch / error helpers).
-#pragma once
+// libh3d.so: the prepare_data entry points (union of the replicate band
+// matrices, size factors of every norm); shares the ctx / scratch / error
+// helpers of h3d_api.hip through h3d_ctx.h.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "h3d.h"
+#include "h3d_ctx.h"
+#include "h3d_errors.h"
+#include "h3d_host.h"
+#include "h3d_kernels.h"
+#include "h3d_prepare.h"
+
+using namespace h3d;
+using namespace h3dint;
+using h3derr::fail;
 
 extern "C" {
 
