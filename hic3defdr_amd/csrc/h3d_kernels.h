@@ -611,11 +611,14 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
     double dc[CM];
 #pragma unroll
     for (int c = 0; c < CM; ++c) dc[c] = (c < C && inb && !wide) ? trow[c] : NAN;
-    double x[M], fv[M], a[M];
+    // counts stay int32 in registers (converted exactly where used): the
+    // M = 24 / 32 instantiations must not spill
+    int32_t x[M];
+    double fv[M], a[M];
 #pragma unroll
     for (int k = 0; k < M; ++k) {
       if (k < R) {
-        x[k] = (double)raw[i * R + k];
+        x[k] = raw[i * R + k];
         fv[k] = f[i * R + k];
         double ak = 0.0;
 #pragma unroll
@@ -623,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
           if (c == cond[k]) ak = dc[c];
         a[k] = wide ? trow[k] : ak;
       } else {
-        x[k] = 0.0;
+        x[k] = 0;
         fv[k] = 1.0;
         a[k] = 1.0;
       }

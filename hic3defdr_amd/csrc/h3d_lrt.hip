@@ -9,6 +9,7 @@
 #include "h3d_ctx.h"
 #include "h3d_errors.h"
 #include "h3d_kernels.h"
+#include "h3d_lrt_group.h"
 
 using namespace h3d;
 using namespace h3dint;
@@ -16,15 +17,23 @@ using h3derr::fail;
 
 namespace {
 
+// R <= 8: one lane per pixel (k_lrt); R > 8: one 8-lane group per pixel
+// (k_lrt8, h3d_lrt_group.h)
 template <int M, int CM>
-void launch_lrt(h3d_ctx* ctx, int grid, const int32_t* raw, const double* f,
+void launch_lrt(h3d_ctx* ctx, const int32_t* raw, const double* f,
                 const int32_t* dist, const double* table, int64_t n, int R,
                 int C, int D, const int32_t* cond, int refit, double* p,
                 double* llr, double* mu0, double* mu1, double* disp,
                 int* flags, int wide) {
-  hipLaunchKernelGGL((k_lrt<M, CM>), dim3(grid), dim3(kBlock), 0, ctx->stream,
-                     raw, f, dist, table, n, R, C, D, cond, refit, p, llr, mu0,
-                     mu1, disp, flags, wide);
+  if constexpr (M <= 8) {
+    hipLaunchKernelGGL((k_lrt<M, CM>), dim3(grid_for(ctx, n, 16)), dim3(kBlock), 0,
+                       ctx->stream, raw, f, dist, table, n, R, C, D, cond, refit, p,
+                       llr, mu0, mu1, disp, flags, wide);
+  } else {
+    hipLaunchKernelGGL((k_lrt8<M, CM>), dim3(grid_for(ctx, n * kGroup, 16)),
+                       dim3(kBlock), 0, ctx->stream, raw, f, dist, table, n, R, C, D,
+                       cond, refit, p, llr, mu0, mu1, disp, flags, wide);
+  }
 }
 
 // wide: disp_table is per pixel AND replicate (n, R) (d_dist must be null)
@@ -53,13 +62,12 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   HIP_TRY(hipMemcpyAsync(d_tab, disp_table, tab_n * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d_cond, cond_of_rep, R * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
-  const int grid = grid_for(ctx, n, 16);
   {
     ProfScope ps(ctx, "lrt", n, 1);
-    const int m = R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : 32;
+    const int m = R <= 4 ? 4 : R <= 8 ? 8 : R <= 16 ? 16 : R <= 24 ? 24 : 32;
     const int cm = C <= 2 ? 2 : C <= 4 ? 4 : 8;
 #define H3D_LRT(MM, CC)                                                          \
-  launch_lrt<MM, CC>(ctx, grid, d_raw, d_f, d_dist, d_tab, n, R, C, D, d_cond,   \
+  launch_lrt<MM, CC>(ctx, d_raw, d_f, d_dist, d_tab, n, R, C, D, d_cond,   \
                      refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, d_fl, wide)
     if (m == 4 && cm == 2) H3D_LRT(4, 2);
     else if (m == 4 && cm == 4) H3D_LRT(4, 4);
@@ -68,6 +76,8 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     else if (m == 16 && cm == 2) H3D_LRT(16, 2);
     else if (m == 16 && cm == 4) H3D_LRT(16, 4);
     else if (m <= 16) H3D_LRT(16, 8);
+    else if (m == 24 && cm <= 4) H3D_LRT(24, 4);
+    else if (m == 24) H3D_LRT(24, 8);
     else H3D_LRT(32, 8);
 #undef H3D_LRT
   }

@@ -53,6 +53,44 @@ H3D_HD double np_sum(const double* v, int n) {
   return NAN;
 }
 
+// np_sum's association fed one value at a time, in index order k = 0..n-1
+// (the same additions in the same order, so the same bits): the caller needs
+// no array of the n values -- 8 accumulators instead of M registers.
+struct NpSumStream {
+  double r[8];
+  double res;
+  int n, blk;
+  H3D_HD explicit NpSumStream(int n_) : res(0.0), n(n_), blk(n_ - n_ % 8) {}
+  H3D_HD void add(int k, double v) {
+    if (n < 8) {
+      res += v;
+    } else if (k < 8) {
+      r[k] = v;
+    } else if (k < blk) {
+      r[k % 8] += v;
+    } else {
+      if (k == blk) res = combine();
+      res += v;
+    }
+  }
+  // the same with a runtime position j (compacted subsets): register
+  // selects instead of an indexed accumulator array (no scratch)
+  H3D_HD void add_dyn(int j, double v) {
+    if (n < 8 || j >= blk) {
+      if (n >= 8 && j == blk) res = combine();
+      res += v;
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (t == (j & 7)) r[t] = (j < 8) ? v : r[t] + v;
+  }
+  H3D_HD double combine() const {
+    return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  }
+  H3D_HD double sum() const { return (n >= 8 && blk == n) ? combine() : res; }
+};
+
 // MLE of mu under fixed per-replicate dispersion: root of
 //   S(mu) = sum_k (x_k - mu b_k) / (mu + a_k mu^2 b_k)      (scaled_nb.py:143-147)
 // over the replicates k < n with bit k of `mask` set.
@@ -61,8 +99,8 @@ H3D_HD double np_sum(const double* v, int n) {
 // theta = log(mu), so the root is unique; here it is found per lane by
 // Newton on g(theta) = mu S(mu) inside a shrinking bracket (bisection
 // safeguard), to full double precision.
-template <int M>
-H3D_HD double fit_mu(const double* x, const double* b, const double* a, int n,
+template <int M, typename TX>
+H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
                      unsigned mask, int* status) {
   double sx = 0.0, init = 0.0;
   int cnt = 0;
@@ -304,58 +342,45 @@ H3D_HD double logpmf(double k, double m, double phi) {
          k * log(m) - k * log(r + m);
 }
 
-// masked mean of n values in order (np.mean of the compacted subset)
-template <int M>
-H3D_HD double np_mean_mask(const double* v, int n, unsigned mask) {
-  int cnt = 0;
-#pragma unroll
-  for (int k = 0; k < M; ++k) cnt += (k < n && ((mask >> k) & 1u)) ? 1 : 0;
-  if (cnt < 8) {
-    double res = 0.0;
-#pragma unroll
-    for (int k = 0; k < M; ++k)
-      if (k < n && ((mask >> k) & 1u)) res += v[k];
-    return res / cnt;
-  }
-  double t[M];  // rare (>= 8 replicates per condition): compact then pairwise
-  int j = 0;
-  for (int k = 0; k < n; ++k)
-    if ((mask >> k) & 1u) t[j++] = v[k];
-  return np_sum<M>(t, cnt) / cnt;
-}
-
 // Per-pixel LRT (lrt.py:7-50). a[k] = disp_wide[k] = disp[cond[k]]; CM is a
 // compile-time bound on the number of conditions C.
-template <int M, int CM>
-H3D_HD int lrt_pixel(const double* x, const double* f, const double* a,
+template <int M, int CM, typename TX>
+H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
                      const int* cond, int R, int C, bool refit, double* p,
                      double* llr, double* mu0, double* mu1) {
   int st = 0;
-  if (refit) {
-    *mu0 = fit_mu<M>(x, f, a, R, ~0u, &st);
-  } else {
-    double q[M];
-#pragma unroll
-    for (int k = 0; k < M; ++k) q[k] = (k < R) ? x[k] / f[k] : 0.0;
-    *mu0 = np_sum<M>(q, R) / R;
-  }
-#pragma unroll
-  for (int c = 0; c < CM; ++c) {
-    if (c >= C) break;
+  // fit 0 is the null (every replicate), fit t = c + 1 condition c's
+  // replicates: ONE runtime loop, so fit_mu is inlined once rather than CM + 1
+  // times (code size and register pressure of the wide-R instantiations)
+#pragma unroll 1
+  for (int t = 0; t <= C; ++t) {
     unsigned mask = 0u;
 #pragma unroll
     for (int k = 0; k < M; ++k)
-      if (k < R && cond[k] == c) mask |= (1u << k);
+      if (k < R && (t == 0 || cond[k] == t - 1)) mask |= (1u << k);
+    double mu;
     if (refit) {
-      mu1[c] = fit_mu<M>(x, f, a, R, mask, &st);
+      mu = fit_mu<M>(x, f, a, R, mask, &st);
     } else {
-      double q[M];
+      // np.mean(raw / f) over the fit's replicates (lrt.py:36-40)
+      int cnt = 0;
 #pragma unroll
-      for (int k = 0; k < M; ++k) q[k] = (k < R) ? x[k] / f[k] : 0.0;
-      mu1[c] = np_mean_mask<M>(q, R, mask);
+      for (int k = 0; k < M; ++k) cnt += (k < R && ((mask >> k) & 1u)) ? 1 : 0;
+      NpSumStream q(cnt);
+      int j = 0;
+#pragma unroll
+      for (int k = 0; k < M; ++k)
+        if (k < R && ((mask >> k) & 1u)) q.add_dyn(j++, (double)x[k] / f[k]);
+      mu = q.sum() / cnt;
     }
+    if (t == 0) *mu0 = mu;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c == t - 1) mu1[c] = mu;
   }
-  double tn[M], ta[M];
+  // the two log-likelihood rows are summed as they are produced
+  // (NpSumStream: numpy's association without the two M-long rows)
+  NpSumStream tn(R), ta(R);
 #pragma unroll
   for (int k = 0; k < M; ++k) {
     if (k < R) {
@@ -367,18 +392,16 @@ H3D_HD int lrt_pixel(const double* x, const double* f, const double* a,
       // evaluates it left to right, so the terms without m form one common
       // prefix, computed once (3 of the 6 lgammas and r log r) -- the same
       // bits as two separate logpmf calls
+      const double xk = (double)x[k];
       const double r = 1.0 / a[k];
-      const double pre =
-          lgam(r + x[k]) - lgam(x[k] + 1) - lgam(r) + r * log(r);
+      const double pre = lgam(r + xk) - lgam(xk + 1) - lgam(r) + r * log(r);
       const double m0k = *mu0 * f[k], m1k = m1 * f[k];
       const double l0 = log(r + m0k), l1 = log(r + m1k);
-      tn[k] = pre - r * l0 + x[k] * log(m0k) - x[k] * l0;
-      ta[k] = pre - r * l1 + x[k] * log(m1k) - x[k] * l1;
-    } else {
-      tn[k] = ta[k] = 0.0;
+      tn.add(k, pre - r * l0 + xk * log(m0k) - xk * l0);
+      ta.add(k, pre - r * l1 + xk * log(m1k) - xk * l1);
     }
   }
-  *llr = np_sum<M>(tn, R) - np_sum<M>(ta, R);
+  *llr = tn.sum() - ta.sum();
   *p = chi2_sf((double)(C - 1), -2 * *llr);
   return st;
 }

@@ -86,6 +86,43 @@ def test_lrt_refit_false_vs_oracle(ctx):
     assert rel_err(m1, rm1) < 1e-14
 
 
+@pytest.mark.parametrize('R,C', [(9, 2), (12, 3), (18, 3), (24, 5), (32, 8)])
+@pytest.mark.parametrize('refit', [True, False])
+def test_lrt_wide_designs_vs_oracle(ctx, R, C, refit):
+    """R > 8 runs k_lrt8 (one 8-lane group per pixel, h3d_lrt_group.h):
+    unequal condition sizes, interleaved replicate order, numpy's tail
+    association (R % 8 != 0) and the compacted means of refit_mu=False."""
+    rng = np.random.default_rng(R * 10 + C)
+    n = 600
+    cond = np.sort(np.r_[np.arange(C), rng.integers(0, C, R - C)])
+    rng.shuffle(cond)
+    design = np.eye(C, dtype=bool)[cond]
+    f = np.exp(rng.normal(0, 0.3, (n, R)))
+    mu = rng.gamma(2.0, 20.0, n)[:, None] * f
+    raw = rng.negative_binomial(10, 10 / (10 + mu)).astype(np.int64)
+    for c in range(C):   # no all-zero condition row (the MLE has no root)
+        first = np.flatnonzero(cond == c)[0]
+        raw[raw[:, cond == c].sum(axis=1) == 0, first] = 1
+    dist = rng.integers(0, 50, n).astype(np.int32)
+    tab = rng.uniform(0.01, 0.3, (50, C))
+    p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, cond, refit_mu=refit)
+    disp_wide = np.dot(tab[dist], design.T)
+    rp, rllr, rm0, rm1 = oracle.lrt(raw, f, disp_wide, design, refit_mu=refit)
+    assert rel_err(p, rp) < RTOL_PQ
+    # llr is a difference of two R-term sums: near 0 its error is absolute
+    # (the MLE tolerance times the slope), measured 7e-14 at |llr| 4e-7
+    np.testing.assert_allclose(llr, rllr, rtol=1e-7, atol=1e-10)
+    tol = RTOL_MU if refit else 1e-14
+    assert rel_err(m0, rm0) < tol
+    assert rel_err(m1, rm1) < tol
+    # lrt.py's own (n, R) dispersion argument: the same numbers, bit for bit
+    wp, wllr, wm0, wm1 = ctx.lrt_wide(raw, f, disp_wide, cond, C,
+                                      refit_mu=refit)
+    np.testing.assert_array_equal(wp, p)
+    np.testing.assert_array_equal(wllr, llr)
+    np.testing.assert_array_equal(wm1, m1)
+
+
 @pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3', 'r16c2'])
 def test_union_and_size_factors_vs_reference(ctx, name):
     g, kw = e2e_inputs(name)
