@@ -29,6 +29,7 @@ EXPORTS = [
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
     'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
+    'h3d_bh_ctx', 'h3d_bh_dev',
 ]
 
 
@@ -90,6 +91,8 @@ def load_library(path=None):
             'h3d_lrt_dev': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I, _I,
                                  _P, _P, _P, _P, _P]),
             'h3d_bh': (_I, [_P, _I64, _P]),
+            'h3d_bh_ctx': (_I, [_P, _P, _I64, _P]),
+            'h3d_bh_dev': (_I, [_P, _P, _I64, _P]),
             'h3d_profile_enable': (_I, [_P, _I]),
             'h3d_profile_read': (_I, [_P, ctypes.c_char_p, _P, _P, _P]),
             'h3d_profile_reset': (_I, [_P]),
@@ -306,6 +309,18 @@ class Context(object):
         _check(self.lib.h3d_cml(self.handle, _ptr(data), n, r,
                                 ctypes.byref(out)), 'h3d_cml')
         return out.value
+
+    def bh(self, pvalues):
+        """BH q-values on this ctx's GPU (h3d_bh_ctx; same bits as bh())."""
+        p = _c(pvalues, np.float64)
+        q = np.empty_like(p)
+        _check(self.lib.h3d_bh_ctx(self.handle, _ptr(p), len(p), _ptr(q)),
+               'h3d_bh_ctx')
+        return q
+
+    def bh_dev(self, d_p, n, d_q):
+        _check(self.lib.h3d_bh_dev(self.handle, _P(d_p), n, _P(d_q)),
+               'h3d_bh_dev')
 
     def lrt_dev(self, d_raw, d_f, d_dist, disp_table, n, R, cond_of_rep,
                 d_p, d_llr, d_mu0, d_mu1, d_disp=None, refit_mu=True):

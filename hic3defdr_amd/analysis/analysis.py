@@ -8,7 +8,7 @@ work runs on the GPU through libh3d.so:
   estimate_disp -> h3d_disp_per_dist (qcml per distance x condition),
                    h3d_disp_table (lowess smoother, host C++ in libh3d)
   lrt           -> h3d_lrt (fused per-pixel NB GLM fits + LRT + chi2)
-  bh            -> h3d_bh
+  bh            -> h3d_bh_ctx (radix sort + reverse min-scan on the GPU)
   threshold / classify / collect
                 -> h3d_find_clusters + h3d_format_clusters (host C++ in
                    libh3d: the reference's DirectedDisjointSet clustering and
@@ -265,14 +265,14 @@ class AnalyzingHiC3DeFDR(object):
                     if self.loop_patterns else None
                 mine[chrom] = self.load_data('pvalues', chrom, idx=li)
             for chrom, q in parallel.distributed_bh(sh, mine,
-                                                    _native.bh).items():
+                                                    self._ctx().bh).items():
                 self.save_data(q, 'qvalues', chrom)
             sh.barrier()
             return
         loop_idx = self.load_data('loop_idx', 'all')[0] \
             if self.loop_patterns else None
         pvalues, offsets = self.load_data('pvalues', 'all', idx=loop_idx)
-        q = _native.bh(pvalues)
+        q = self._ctx().bh(pvalues)
         for i, chrom in enumerate(self.chroms):
             self.save_data(q[offsets[i]:offsets[i + 1]], 'qvalues', chrom)
 

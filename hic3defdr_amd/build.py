@@ -34,9 +34,10 @@ ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 # (source, compiler): device TUs through hipcc, host-only TUs through g++
 NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_lrt.hip', 'hipcc'),
                ('h3d_prepare_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
+               ('h3d_bh.hip', 'hipcc'),
                ('h3d_calls.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
-           'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h']
+           'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h', 'h3d_lrt_group.h']
 # concurrent compiles (each hipcc TU is single-threaded; the box sets
 # MAX_JOBS=16, this container has 8 CPUs)
 JOBS = max(1, min(int(os.environ.get('MAX_JOBS', '8')), os.cpu_count() or 1))

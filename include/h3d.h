@@ -18,7 +18,7 @@
  *   h3d_lrt                <- util/lrt.py:7-50 (+ analysis/analysis.py:272-278)
  *   h3d_lrt_wide           <- util/lrt.py:7 lrt(raw, f, disp, design) as called
  *   h3d_cml                <- util/dispersion.py:46-80 cml
- *   h3d_bh                 <- analysis/analysis.py:286-303 (lib5c
+ *   h3d_bh / _ctx / _dev   <- analysis/analysis.py:286-303 (lib5c
  *                              adjust_pvalues = BH)
  *   h3d_find_clusters      <- util/clusters.py:73-97 find_clusters (threshold /
  *                              classify, analysis.py:366-486)
@@ -179,8 +179,16 @@ int h3d_cml(h3d_ctx* ctx, const double* data, int64_t n, int r, double* disp);
 
 /* ---- bh ---------------------------------------------------------------- */
 
-/* Benjamini-Hochberg q-values over the finite p-values (NaN elsewhere). */
+/* Benjamini-Hochberg q-values over the finite p-values (NaN elsewhere), on
+ * the host CPU (no ctx). */
 int h3d_bh(const double* p, int64_t n, double* q);
+
+/* The same on the ctx's GPU: one radix sort of (p, index), the ratio
+ * p_(j) / ((j + 1) / m), a reverse min-scan, a scatter -- bit-identical to
+ * h3d_bh. _ctx: host buffers (synchronous); _dev: device buffers, stream-
+ * ordered on the ctx stream (n < 2^31). */
+int h3d_bh_ctx(h3d_ctx* ctx, const double* p, int64_t n, double* q);
+int h3d_bh_dev(h3d_ctx* ctx, const double* d_p, int64_t n, double* d_q);
 
 /* ---- threshold / classify / collect (host) ------------------------------ */
 

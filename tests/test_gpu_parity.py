@@ -211,3 +211,22 @@ def test_disp_dev_with_noop_reduce_matches_single_rank(ctx):
     np.testing.assert_allclose(one, multi, rtol=1e-7, atol=1e-12)
     np.testing.assert_allclose(multi, g['disp_per_dist'], rtol=RTOL_DISP,
                                atol=1e-12)
+
+
+@pytest.mark.parametrize('case', ['random', 'ties', 'nan', 'one', 'allnan',
+                                  'empty', 'large'])
+def test_bh_gpu_bit_identical(ctx, case):
+    """h3d_bh_ctx (GPU radix sort + min-scan) == h3d_bh (host) == the
+    oracle's statsmodels fdrcorrection restatement, bit for bit."""
+    from hic3defdr_amd import _native
+    rng = np.random.default_rng(7)
+    p = {'random': rng.random(10007),
+         'ties': np.round(rng.random(5000), 2),
+         'nan': np.where(rng.random(3000) < 0.2, np.nan, rng.random(3000)),
+         'one': np.array([0.3]),
+         'allnan': np.full(17, np.nan),
+         'empty': np.empty(0),
+         'large': rng.random(3_000_000) ** 3}[case]
+    q = ctx.bh(p)
+    np.testing.assert_array_equal(q, _native.bh(p))
+    np.testing.assert_array_equal(q, oracle.adjust_pvalues(p))
