@@ -353,7 +353,57 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     int end_bit = 1;
     while ((1 << end_bit) <= D) ++end_bit;
     size_t tmp_bytes = 0;
-    if (ctx->disp_sort == 1 && end_bit <= 16) {
+    if (ctx->disp_sort == 2) {
+      // one (distance, max, min count) order per condition (k_gather_soa_cond)
+      idx_out = (int32_t*)scratch(ctx, "idx_out_c", (size_t)C * n * 4);
+      int32_t* d_cor = (int32_t*)scratch(ctx, "sort_cond_of_rep", R * 4);
+      int32_t* d_reps = (int32_t*)scratch(ctx, "sort_reps", (size_t)C * kMaxReps * 4);
+      if (!idx_out || !d_cor || !d_reps) return fail(H3D_ENOMEM, "sort buffers");
+      HIP_TRY(hipMemcpyAsync(d_cor, cond_of_rep, R * 4, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(d_reps, rep_idx.data(), (size_t)C * kMaxReps * 4,
+                             hipMemcpyHostToDevice, s));
+      const bool k32 = end_bit <= 16;
+      const int cbits = k32 ? 32 - end_bit : 64 - end_bit;
+      void* keys = scratch(ctx, "dkeys", n * (k32 ? 4 : 8));
+      void* keys_s = scratch(ctx, "dkeys_s", n * (k32 ? 4 : 8));
+      if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
+      for (int c = 0; c < C; ++c) {
+        int32_t* perm = idx_out + (size_t)c * n;
+        if (k32) {
+          hipLaunchKernelGGL(k_dist_cond_keys<uint32_t>, dim3(grid_for(ctx, n)),
+                             dim3(kBlock), 0, s, d_dist, d_raw, n, R,
+                             d_reps + c * kMaxReps, nrep[c], cbits, (uint32_t*)keys);
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)keys,
+                                                     (uint32_t*)keys_s, idx_in, perm,
+                                                     (int)n, 0, 32, s));
+          void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+          if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)keys,
+                                                     (uint32_t*)keys_s, idx_in, perm,
+                                                     (int)n, 0, 32, s));
+          if (c == 0)
+            hipLaunchKernelGGL(k_key_dist<uint32_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
+                               0, s, (const uint32_t*)keys_s, n, cbits, dist_s);
+        } else {
+          hipLaunchKernelGGL(k_dist_cond_keys<uint64_t>, dim3(grid_for(ctx, n)),
+                             dim3(kBlock), 0, s, d_dist, d_raw, n, R,
+                             d_reps + c * kMaxReps, nrep[c], cbits, (uint64_t*)keys);
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint64_t*)keys,
+                                                     (uint64_t*)keys_s, idx_in, perm,
+                                                     (int)n, 0, 64, s));
+          void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
+          if (!tmp) return fail(H3D_ENOMEM, "sort temp");
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint64_t*)keys,
+                                                     (uint64_t*)keys_s, idx_in, perm,
+                                                     (int)n, 0, 64, s));
+          if (c == 0)
+            hipLaunchKernelGGL(k_key_dist<uint64_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
+                               0, s, (const uint64_t*)keys_s, n, cbits, dist_s);
+        }
+      }
+      hipLaunchKernelGGL(k_gather_soa_cond, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         idx_out, d_cor, d_raw, d_f, n, R, raw_s, f_s);
+    } else if (ctx->disp_sort == 1 && end_bit <= 16) {
       // (distance, total count) keys: same segments, less lane divergence;
       // 32-bit keys (16 count bits) whenever the distance fits 16 bits
       constexpr int cbits = 16;
@@ -395,8 +445,9 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
                                                  idx_out, (int)n, 0, end_bit, s));
     }
-    hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                       idx_out, d_raw, d_f, n, R, raw_s, f_s);
+    if (ctx->disp_sort != 2)
+      hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                         idx_out, d_raw, d_f, n, R, raw_s, f_s);
     hipLaunchKernelGGL(k_seg_bounds, dim3((D + 1 + 255) / 256), dim3(256), 0, s,
                        dist_s, n, D, d_seg);
     HIP_TRY(hipMemcpyAsync(seg_start.data(), d_seg, (D + 1) * 8,

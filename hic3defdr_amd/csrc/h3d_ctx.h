@@ -79,7 +79,11 @@ struct h3d_ctx {
   // 1 (distance, total count)
   int disp_w = 4;  // measured best (sweep at 7413b12, equalize ms/step for
                    // W 1/2/3/4: 10.7 / 10.55 / 9.76 / 9.62)
-  int disp_sort = 1;  // measured: 55.6 ms unsorted -> 52.5 ms sorted
+  // H3D_DISP_SORT: pixel order inside a distance segment. 0 position, 1
+  // (total count) -- r01: 55.6 -> 52.5 ms --, 2 one (max, min count) order
+  // per condition -- r02 cfg2: equalize 7.62 -> 5.68 ms, 277 -> 311 Mpx/s;
+  // cfg4 equalize 118 -> 111 ms (profiles/r02/sortab)
+  int disp_sort = 2;
   int nll_w = 1;  // H3D_NLL_W: min waves/SIMD of the NLL-only pass (1, 2, 4)
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
                     // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)

@@ -103,6 +103,54 @@ static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
   }
 }
 
+// AoS (n, R) -> SoA [r][i] with one pixel order PER CONDITION: replicate r
+// is gathered through perm[cond_of_rep[r] * n + i]. Sound because every
+// consumer of a condition's SoA rows (equalize, the NLL, the segment sums)
+// touches only that condition's replicates, and all orders share the same
+// distance segments.
+static __global__ void k_gather_soa_cond(const int32_t* __restrict__ perm,
+                                         const int32_t* __restrict__ cond_of_rep,
+                                         const int32_t* __restrict__ raw,
+                                         const double* __restrict__ f, int64_t n,
+                                         int R, int32_t* __restrict__ raw_s,
+                                         double* __restrict__ f_s) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    for (int r = 0; r < R; ++r) {
+      const int64_t src = perm[(int64_t)cond_of_rep[r] * n + i];
+      raw_s[(int64_t)r * n + i] = raw[src * R + r];
+      f_s[(int64_t)r * n + i] = f[src * R + r];
+    }
+}
+
+// per-condition sort key (distance, max count, min count over the
+// condition's replicates; each capped to its half of the cbits count bits).
+// Modelled on the cfg2 census (tools/order_experiment.py): wave lane
+// utilisation of the equalize pass 0.68 with the total-count key -> 0.79.
+template <typename K>
+__global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
+                                 const int32_t* __restrict__ raw, int64_t n, int R,
+                                 const int32_t* __restrict__ reps, int nr, int cbits,
+                                 K* __restrict__ keys) {
+  const int lo = cbits / 2, hi = cbits - lo;
+  const uint64_t cap_lo = (1ull << lo) - 1ull, cap_hi = (1ull << hi) - 1ull;
+  const uint64_t dcap = (uint64_t)(K)~(K)0 >> cbits;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t mx = 0, mn = ~0ull;
+    for (int j = 0; j < nr; ++j) {
+      const uint64_t v = (uint32_t)raw[i * R + reps[j]];
+      mx = v > mx ? v : mx;
+      mn = v < mn ? v : mn;
+    }
+    if (mx > cap_hi) mx = cap_hi;
+    if (mn > cap_lo) mn = cap_lo;
+    uint64_t d = (uint32_t)dist[i];
+    if (d > dcap) d = dcap;
+    keys[i] = (K)((d << cbits) | (mx << lo) | mn);
+  }
+}
+
 // sort key (distance, total count capped to cbits bits): inside a distance
 // segment pixels of similar depth sit in the same wave, so the q2qnbinom
 // branches (tail side, series vs continued fraction) diverge less. The count
