@@ -95,6 +95,9 @@ constexpr int kLaunchBlock = 256;
 
 // grow-only device buffer of the ctx, by slot name (nullptr on OOM)
 void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes);
+// the same, but a grown buffer keeps its first `keep` bytes (stream-ordered
+// copy; growth at least doubles the capacity)
+void* scratch_keep(h3d_ctx* ctx, const char* slot, size_t bytes, size_t keep);
 hipEvent_t ev_get(h3d_ctx* ctx);
 // folds the recorded event pairs into ctx->stats (synchronises the stream)
 void prof_collect(h3d_ctx* ctx);

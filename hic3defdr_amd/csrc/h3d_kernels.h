@@ -65,12 +65,18 @@ static __global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
     out[i] = (int32_t)i;
 }
 
-// AoS (n, R) -> distance-sorted SoA [r][i]
+// destination row of every replicate (a kernel argument by value): the SoA
+// row of replicate r is raw[r][i] / f[r][i]
+struct SoaRows {
+  int32_t* raw[kMaxReps];
+  double* f[kMaxReps];
+};
+
+// AoS (n, R) -> distance-sorted SoA rows
 static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
-                             const int32_t* __restrict__ raw,
-                             const double* __restrict__ f, int64_t n, int R,
-                             int32_t* __restrict__ raw_s,
-                             double* __restrict__ f_s) {
+                                    const int32_t* __restrict__ raw,
+                                    const double* __restrict__ f, int64_t n, int R,
+                                    SoaRows dst) {
   if (R == 4 && ((uintptr_t)raw & 15) == 0 && ((uintptr_t)f & 15) == 0) {
     // the common shape: one 16 B load of the raw row, two 16 B loads of the
     // f row per pixel (rows are 16 B aligned), so the random row gather
@@ -82,14 +88,14 @@ static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
       const int64_t src = perm[i];
       const int4 rv = raw4[src];
       const double2 fa = f2[2 * src], fb = f2[2 * src + 1];
-      raw_s[i] = rv.x;
-      raw_s[n + i] = rv.y;
-      raw_s[2 * n + i] = rv.z;
-      raw_s[3 * n + i] = rv.w;
-      f_s[i] = fa.x;
-      f_s[n + i] = fa.y;
-      f_s[2 * n + i] = fb.x;
-      f_s[3 * n + i] = fb.y;
+      dst.raw[0][i] = rv.x;
+      dst.raw[1][i] = rv.y;
+      dst.raw[2][i] = rv.z;
+      dst.raw[3][i] = rv.w;
+      dst.f[0][i] = fa.x;
+      dst.f[1][i] = fa.y;
+      dst.f[2][i] = fb.x;
+      dst.f[3][i] = fb.y;
     }
     return;
   }
@@ -97,41 +103,47 @@ static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t src = perm[i];
     for (int r = 0; r < R; ++r) {
-      raw_s[(int64_t)r * n + i] = raw[src * R + r];
-      f_s[(int64_t)r * n + i] = f[src * R + r];
+      dst.raw[r][i] = raw[src * R + r];
+      dst.f[r][i] = f[src * R + r];
     }
   }
 }
 
-// AoS (n, R) -> SoA [r][i] with one pixel order PER CONDITION: replicate r
-// is gathered through perm[cond_of_rep[r] * n + i]. Sound because every
-// consumer of a condition's SoA rows (equalize, the NLL, the segment sums)
-// touches only that condition's replicates, and all orders share the same
-// distance segments.
-static __global__ void k_gather_soa_cond(const int32_t* __restrict__ perm,
-                                         const int32_t* __restrict__ cond_of_rep,
-                                         const int32_t* __restrict__ raw,
-                                         const double* __restrict__ f, int64_t n,
-                                         int R, int32_t* __restrict__ raw_s,
-                                         double* __restrict__ f_s) {
+// one condition's SoA rows re-ordered inside their distance segments:
+// raw_s[reps[j]][i] = src_raw[j][perm[i]] (perm maps within segments, so the
+// reads stay inside a segment's window -- L2-resident, unlike a second random
+// gather of the AoS rows). One pixel order PER CONDITION is sound because
+// every consumer of a condition's SoA rows (equalize, the NLL, the segment
+// sums) touches only that condition's replicates, and all orders share the
+// same distance segments.
+static __global__ void k_permute_rows(const int32_t* __restrict__ perm,
+                                      const int32_t* __restrict__ src_raw,
+                                      const double* __restrict__ src_f,
+                                      const int32_t* __restrict__ reps, int nr, int64_t n,
+                                      int32_t* __restrict__ raw_s,
+                                      double* __restrict__ f_s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    for (int r = 0; r < R; ++r) {
-      const int64_t src = perm[(int64_t)cond_of_rep[r] * n + i];
-      raw_s[(int64_t)r * n + i] = raw[src * R + r];
-      f_s[(int64_t)r * n + i] = f[src * R + r];
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t src = perm[i];
+    for (int j = 0; j < nr; ++j) {
+      raw_s[(int64_t)reps[j] * n + i] = src_raw[(int64_t)j * n + src];
+      f_s[(int64_t)reps[j] * n + i] = src_f[(int64_t)j * n + src];
     }
+  }
 }
 
 // per-condition sort key (distance, max count, min count over the
 // condition's replicates; each capped to its half of the cbits count bits).
 // Modelled on the cfg2 census (tools/order_experiment.py): wave lane
 // utilisation of the equalize pass 0.68 with the total-count key -> 0.79.
+// soa = 0: raw is the AoS (n, R) input (replicates reps[0..nr)); soa = 1: raw
+// is the condition's nr consecutive SoA rows [j][i] in an earlier order, dist
+// the matching distances -- coalesced reads.
 template <typename K>
 __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
                                  const int32_t* __restrict__ raw, int64_t n, int R,
                                  const int32_t* __restrict__ reps, int nr, int cbits,
-                                 K* __restrict__ keys) {
+                                 int soa, K* __restrict__ keys) {
   const int lo = cbits / 2, hi = cbits - lo;
   const uint64_t cap_lo = (1ull << lo) - 1ull, cap_hi = (1ull << hi) - 1ull;
   const uint64_t dcap = (uint64_t)(K)~(K)0 >> cbits;
@@ -139,7 +151,7 @@ __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
        i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t mx = 0, mn = ~0ull;
     for (int j = 0; j < nr; ++j) {
-      const uint64_t v = (uint32_t)raw[i * R + reps[j]];
+      const uint64_t v = (uint32_t)(soa ? raw[(int64_t)j * n + i] : raw[i * R + reps[j]]);
       mx = v > mx ? v : mx;
       mn = v < mn ? v : mn;
     }

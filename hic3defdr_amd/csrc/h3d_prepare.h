@@ -3,13 +3,14 @@
 // distance-conditional median-of-ratios size factors (util/scaling.py:68-127,
 // util/binning.py:4-25).
 //
-// Union: every stored entry of every replicate becomes a 64-bit key
-// row * n_bins + col (or a sentinel when it is outside 0 <= col-row <=
-// dist_max, on a bin with zero bias, or zero); one radix sort of (key, entry)
-// groups a pixel's replicate entries into a run; a run is kept when the sum
-// of its deconvoluted values is finite and > 0 (the reference drops zero sums
-// and filters isfinite/>= mean_thresh*R = 0). Keys sort lexicographically in
-// (row, col): the reference's order (csr sum -> tocoo).
+// Union: every in-band non-zero entry of every replicate is staged (compacted
+// per replicate, so scratch and the 2^31 cap follow the band) as a 64-bit key
+// row * n_bins + col; one radix sort of (key, entry) groups a pixel's
+// replicate entries into a run; a run is kept when the sum of its
+// deconvoluted values (inverse bias 0 on zero-bias bins) is finite and > 0
+// (the reference drops zero sums and filters isfinite / >= mean_thresh*R = 0).
+// Keys sort lexicographically in (row, col): the reference's order (csr sum
+// -> tocoo).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,28 +31,47 @@ static __global__ void k_csr_rows(const int64_t* __restrict__ indptr, int n_bins
   for (int64_t j = indptr[i]; j < indptr[i + 1]; ++j) row_of[j] = i;
 }
 
+// entries staged for the union: in the band (0 <= col - row <= dist_max) and
+// non-zero -- wipe_distances' survivors (util/matrices.py:41-62). Zero-bias
+// bins are NOT dropped here: the reference's raw gather reads the raw matrix
+// at every union pixel (analysis.py:91-95), so a replicate whose bias is 0 at
+// a pixel another replicate put in the union still reports its count (and
+// balanced v / 0 = inf); k_run_keep decides union membership.
+__device__ inline bool union_stage(int i, int c, double v, int n_bins, int dist_max) {
+  const int d = c - i;
+  return (d >= 0) && (d <= dist_max) && (c < n_bins) && (v != 0.0);
+}
+
+static __global__ void k_union_flags(const int32_t* __restrict__ row_of,
+                                     const int32_t* __restrict__ col,
+                                     const double* __restrict__ val, int64_t n_ent,
+                                     int n_bins, int dist_max,
+                                     int32_t* __restrict__ flag) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_ent;
+       j += (int64_t)gridDim.x * blockDim.x)
+    flag[j] = union_stage(row_of[j], col[j], val[j], n_bins, dist_max) ? 1 : 0;
+}
+
+// the kept entries of one replicate, compacted to ent_offset + pos[j]
+// (pos = exclusive scan of the flags): only in-band entries are staged
 static __global__ void k_union_keys(const int32_t* __restrict__ row_of,
-                             const int32_t* __restrict__ col,
-                             const double* __restrict__ val, int64_t n_ent,
-                             int64_t ent_offset, int rep, int R, int n_bins,
-                             int dist_max, const double* __restrict__ bias,
-                             int64_t sentinel, int64_t* __restrict__ keys,
-                             int32_t* __restrict__ ent_idx,
-                             int32_t* __restrict__ ent_rep,
-                             double* __restrict__ ent_val) {
+                                    const int32_t* __restrict__ col,
+                                    const double* __restrict__ val,
+                                    const int32_t* __restrict__ flag,
+                                    const int32_t* __restrict__ pos, int64_t n_ent,
+                                    int64_t ent_offset, int rep, int n_bins,
+                                    int64_t* __restrict__ keys,
+                                    int32_t* __restrict__ ent_idx,
+                                    int32_t* __restrict__ ent_rep,
+                                    double* __restrict__ ent_val) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_ent;
        j += (int64_t)gridDim.x * blockDim.x) {
-    const int i = row_of[j];
-    const int c = col[j];
-    const double v = val[j];
-    const int d = c - i;
-    bool keep = (d >= 0) && (d <= dist_max) && (c < n_bins) && (v != 0.0);
-    if (keep) keep = bias[(int64_t)i * R + rep] != 0.0 && bias[(int64_t)c * R + rep] != 0.0;
-    const int64_t g = ent_offset + j;
-    keys[g] = keep ? (int64_t)i * n_bins + c : sentinel;
+    if (!flag[j]) continue;
+    const int64_t g = ent_offset + pos[j];
+    keys[g] = (int64_t)row_of[j] * n_bins + col[j];
     ent_idx[g] = (int32_t)g;
     ent_rep[g] = rep;
-    ent_val[g] = v;
+    ent_val[g] = val[j];
   }
 }
 
@@ -92,7 +112,10 @@ static __global__ void k_run_keep(const int64_t* __restrict__ keys,
     for (int64_t j = b; j < n_ent && keys[j] == key; ++j) {
       const int e = ent_sorted[j];
       const int rep = ent_rep[e];
-      const double bi = 1.0 / bias[i * R + rep], bc = 1.0 / bias[c * R + rep];
+      // deconvolute(invert=True) (matrices.py:8-38): inverse bias 0 where
+      // the bias is 0, so such entries add nothing to the union total
+      const double b_i = bias[i * R + rep], b_c = bias[c * R + rep];
+      const double bi = b_i == 0.0 ? 0.0 : 1.0 / b_i, bc = b_c == 0.0 ? 0.0 : 1.0 / b_c;
       tot += (bi * ent_val[e]) * bc;
     }
     keep[r] = (tot > 0.0 && tot - tot == 0.0) ? 1 : 0;

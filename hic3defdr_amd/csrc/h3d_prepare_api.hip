@@ -34,58 +34,83 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
   P = PrepUnion();
   P.R = R;
   P.n_bins = n_bins;
-  int64_t tot = 0;
+  int64_t max_m = 0;
   for (int r = 0; r < R; ++r) {
     if (nnz[r] < 0 || (nnz[r] > 0 && (!indices[r] || !data[r])) || !indptr[r])
       return fail(H3D_EARG, "replicate %d CSR", r);
     if (indptr[r][n_bins] != nnz[r]) return fail(H3D_EARG, "replicate %d indptr[-1] != nnz", r);
-    tot += nnz[r];
+    if (nnz[r] >= ((int64_t)1 << 31)) return fail(H3D_EARG, "replicate %d: too many entries", r);
+    max_m = std::max(max_m, nnz[r]);
   }
-  if (tot >= ((int64_t)1 << 31)) return fail(H3D_EARG, "too many entries");
-  P.n_entries = tot;
   const int64_t sentinel = (int64_t)n_bins * n_bins;
   int end_bit = 1;
   while (end_bit < 63 && (((int64_t)1) << end_bit) <= sentinel) ++end_bit;
+  // per-replicate staging (reused): only the in-band entries reach the
+  // per-entry key / sort / scan buffers, so their size and the 2^31 cap
+  // follow the band, not the whole-chromosome nnz
+  const size_t mm = (size_t)std::max<int64_t>(max_m, 1);
   double* d_bias = (double*)scratch(ctx, "u_bias", (size_t)n_bins * R * 8);
   int64_t* d_indptr = (int64_t*)scratch(ctx, "u_indptr", (size_t)(n_bins + 1) * 8);
-  int32_t* d_row = (int32_t*)scratch(ctx, "u_row_of", std::max<int64_t>(tot, 1) * 4);
-  int32_t* d_col = (int32_t*)scratch(ctx, "u_col", std::max<int64_t>(tot, 1) * 4);
-  double* d_val = (double*)scratch(ctx, "u_val_in", std::max<int64_t>(tot, 1) * 8);
-  int64_t* d_keys = (int64_t*)scratch(ctx, "u_keys", std::max<int64_t>(tot, 1) * 8);
-  int32_t* d_ent = (int32_t*)scratch(ctx, "u_ent", std::max<int64_t>(tot, 1) * 4);
-  P.keys_sorted = (int64_t*)scratch(ctx, "u_keys_s", std::max<int64_t>(tot, 1) * 8);
-  P.ent_sorted = (int32_t*)scratch(ctx, "u_ent_s", std::max<int64_t>(tot, 1) * 4);
-  P.ent_rep = (int32_t*)scratch(ctx, "u_ent_rep", std::max<int64_t>(tot, 1) * 4);
-  P.ent_val = (double*)scratch(ctx, "u_ent_val", std::max<int64_t>(tot, 1) * 8);
-  int32_t* d_head = (int32_t*)scratch(ctx, "u_head", std::max<int64_t>(tot, 1) * 4);
-  P.run_of = (int32_t*)scratch(ctx, "u_run_incl", std::max<int64_t>(tot, 1) * 4);
-  if (!d_bias || !d_indptr || !d_row || !d_col || !d_val || !d_keys || !d_ent ||
-      !P.keys_sorted || !P.ent_sorted || !P.ent_rep || !P.ent_val || !d_head || !P.run_of)
-    return fail(H3D_ENOMEM, "union scratch");
+  int32_t* d_row = (int32_t*)scratch(ctx, "u_row_of", mm * 4);
+  int32_t* d_col = (int32_t*)scratch(ctx, "u_col", mm * 4);
+  double* d_val = (double*)scratch(ctx, "u_val_in", mm * 8);
+  int32_t* d_flag = (int32_t*)scratch(ctx, "u_flag", mm * 4);
+  int32_t* d_pos = (int32_t*)scratch(ctx, "u_pos", mm * 4);
+  int32_t* d_cnt = (int32_t*)scratch(ctx, "u_cnt", 4);
+  if (!d_bias || !d_indptr || !d_row || !d_col || !d_val || !d_flag || !d_pos || !d_cnt)
+    return fail(H3D_ENOMEM, "union staging");
   P.bias = d_bias;
   HIP_TRY(hipMemcpyAsync(d_bias, bias, (size_t)n_bins * R * 8, hipMemcpyHostToDevice, s));
-  int64_t off = 0;
+  int64_t tot = 0;  // kept entries so far
+  int64_t* d_keys = nullptr;
+  int32_t* d_ent = nullptr;
   for (int r = 0; r < R; ++r) {
     const int64_t m = nnz[r];
+    if (m == 0) continue;
     HIP_TRY(hipMemcpyAsync(d_indptr, indptr[r], (size_t)(n_bins + 1) * 8, hipMemcpyHostToDevice, s));
-    if (m > 0) {
-      HIP_TRY(hipMemcpyAsync(d_col, indices[r], m * 4, hipMemcpyHostToDevice, s));
-      HIP_TRY(hipMemcpyAsync(d_val, data[r], m * 8, hipMemcpyHostToDevice, s));
-      hipLaunchKernelGGL(k_csr_rows, dim3((n_bins + 255) / 256), dim3(256), 0, s,
-                         d_indptr, n_bins, d_row);
-      hipLaunchKernelGGL(k_union_keys, dim3(grid_for(ctx, m)), dim3(kBlock), 0, s,
-                         d_row, d_col, d_val, m, off, r, R, n_bins, dist_max, d_bias,
-                         sentinel, d_keys, d_ent, P.ent_rep, P.ent_val);
-    }
+    HIP_TRY(hipMemcpyAsync(d_col, indices[r], m * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_val, data[r], m * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_csr_rows, dim3((n_bins + 255) / 256), dim3(256), 0, s,
+                       d_indptr, n_bins, d_row);
+    hipLaunchKernelGGL(k_union_flags, dim3(grid_for(ctx, m)), dim3(kBlock), 0, s, d_row,
+                       d_col, d_val, m, n_bins, dist_max, d_flag);
+    size_t tbs = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tbs, d_flag, d_pos, (int)m, s));
+    void* tmps = scratch(ctx, "cub_tmp_s", tbs);
+    if (!tmps) return fail(H3D_ENOMEM, "scan temp");
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmps, tbs, d_flag, d_pos, (int)m, s));
+    int32_t last[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&last[0], d_pos + m - 1, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last[1], d_flag + m - 1, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t kept = (int64_t)last[0] + last[1];
+    if (tot + kept >= ((int64_t)1 << 31)) return fail(H3D_EARG, "too many in-band entries");
+    // the kept-entry arrays grow (keeping what earlier replicates wrote)
+    const size_t need = (size_t)std::max<int64_t>(tot + kept, 1);
+    d_keys = (int64_t*)scratch_keep(ctx, "u_keys", need * 8, tot * 8);
+    d_ent = (int32_t*)scratch_keep(ctx, "u_ent", need * 4, tot * 4);
+    P.ent_rep = (int32_t*)scratch_keep(ctx, "u_ent_rep", need * 4, tot * 4);
+    P.ent_val = (double*)scratch_keep(ctx, "u_ent_val", need * 8, tot * 8);
+    if (!d_keys || !d_ent || !P.ent_rep || !P.ent_val) return fail(H3D_ENOMEM, "union entries");
+    hipLaunchKernelGGL(k_union_keys, dim3(grid_for(ctx, m)), dim3(kBlock), 0, s, d_row, d_col,
+                       d_val, d_flag, d_pos, m, tot, r, n_bins, d_keys, d_ent, P.ent_rep,
+                       P.ent_val);
     // the staging buffers are reused by the next replicate
     HIP_TRY(hipStreamSynchronize(s));
-    off += m;
+    tot += kept;
   }
+  P.n_entries = tot;
   if (tot == 0) {
     P.n_px = 0;
     *n_px_out = 0;
     return 0;
   }
+  P.keys_sorted = (int64_t*)scratch(ctx, "u_keys_s", tot * 8);
+  P.ent_sorted = (int32_t*)scratch(ctx, "u_ent_s", tot * 4);
+  int32_t* d_head = (int32_t*)scratch(ctx, "u_head", tot * 4);
+  P.run_of = (int32_t*)scratch(ctx, "u_run_incl", tot * 4);
+  if (!P.keys_sorted || !P.ent_sorted || !d_head || !P.run_of)
+    return fail(H3D_ENOMEM, "union scratch");
   size_t tb = 0;
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_keys, P.keys_sorted, d_ent,
                                              P.ent_sorted, (int)tot, 0, end_bit, s));

@@ -230,3 +230,36 @@ def test_bh_gpu_bit_identical(ctx, case):
     q = ctx.bh(p)
     np.testing.assert_array_equal(q, _native.bh(p))
     np.testing.assert_array_equal(q, oracle.adjust_pvalues(p))
+
+
+def test_union_whole_matrix_keeps_only_the_band(ctx):
+    """Whole-chromosome CSRs (entries at every distance, both triangles,
+    explicit zeros, zero-bias bins): only in-band entries are staged on the
+    device, and the union equals the reference's
+    wipe_distances + sum (oracle.sparse_union)."""
+    rng = np.random.default_rng(11)
+    n_bins, R, dmax = 400, 3, 12
+    mats = []
+    for r in range(R):
+        m = sparse.random(n_bins, n_bins, density=0.08, random_state=r + 1,
+                          data_rvs=lambda k: rng.integers(0, 6, k)).tocsr()
+        m.sort_indices()
+        mats.append(m)
+    bias = np.exp(rng.normal(0, 0.2, (n_bins, R)))
+    bias[rng.random((n_bins, R)) < 0.03] = 0.0
+    row, col, raw, bal = ctx.sparse_union(mats, bias, dmax)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        rr, rc = oracle.sparse_union(mats, dist_thresh=dmax,
+                                     bias=bias.copy())
+    np.testing.assert_array_equal(row, rr)
+    np.testing.assert_array_equal(col, rc)
+    dense = np.stack([m.toarray()[row, col] for m in mats], axis=1)
+    # the reference gathers raw at every union pixel whatever the replicate's
+    # bias there (analysis.py:91-101): counts on zero-bias bins stay, and
+    # balanced is v / 0 = inf (or 0 / 0 = nan) exactly as numpy divides
+    np.testing.assert_array_equal(raw, dense)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        bal_ref = dense / (bias[row] * bias[col])
+    np.testing.assert_array_equal(bal, bal_ref)
+    assert np.any(np.isinf(bal)) and np.any(bias[row] * bias[col] == 0)
+    assert np.all((col - row >= 0) & (col - row <= dmax))
