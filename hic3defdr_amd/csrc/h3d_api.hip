@@ -157,7 +157,13 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, \
                        st, seg_flags, list, meta, partial);                         \
   } while (0)
-    if constexpr (M == 4) {
+    if constexpr (M == 2) {
+      // H3D_DISP_W2: the R_c <= 2 path (cfg2's 2 + 2 design)
+      if (ctx->disp_w2 == 8) H3D_EQ(8);
+      else if (ctx->disp_w2 == 6) H3D_EQ(6);
+      else if (ctx->disp_w2 == 5) H3D_EQ(5);
+      else H3D_EQ(4);
+    } else if constexpr (M == 4) {
       if (ctx->disp_w == 4) H3D_EQ(4);
       else if (ctx->disp_w == 3) H3D_EQ(3);
       else if (ctx->disp_w == 2) H3D_EQ(2);
@@ -266,6 +272,8 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_DISP_SORT")) ctx->disp_sort = std::atoi(e);
   if (const char* e = std::getenv("H3D_NLL_W")) ctx->nll_w = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W8")) ctx->disp_w8 = std::atoi(e);
+  if (const char* e = std::getenv("H3D_DISP_W2")) ctx->disp_w2 = std::atoi(e);
+  if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
@@ -591,7 +599,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                      d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
   if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 16, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
-  const int mslot = maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32;
+  const int mslot = (maxnr <= 2 && ctx->disp_m2) ? 2 : maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32;
   int rounds = 0, batch = 2, rc = 0;
   if (!reduce) {
     // Single rank: one equalize pass per qcml iteration over every segment
@@ -610,7 +618,8 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   launch_disp_work<MM, false>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C,     \
                               d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial); \
   launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
-        if (mslot == 4) { H3D_QCML_ITER(4); }
+        if (mslot == 2) { H3D_QCML_ITER(2); }
+        else if (mslot == 4) { H3D_QCML_ITER(4); }
         else if (mslot == 8) { H3D_QCML_ITER(8); }
         else if (mslot == 16) { H3D_QCML_ITER(16); }
         else { H3D_QCML_ITER(32); }

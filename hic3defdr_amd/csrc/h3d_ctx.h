@@ -85,6 +85,12 @@ struct h3d_ctx {
   // cfg4 equalize 118 -> 111 ms (profiles/r02/sortab)
   int disp_sort = 2;
   int nll_w = 1;  // H3D_NLL_W: min waves/SIMD of the NLL-only pass (1, 2, 4)
+  // H3D_DISP_M2 / _W2: the M = 2 instantiation for R_c <= 2 and its
+  // equalize register budget. r02 cfg2 (10 steps, two runs): M = 4 305 / 316
+  // Mpx/s; M = 2 at W 4 / 5 / 6: 320 (327) / 317 / 307 -- the gain is
+  // k_brent<2> (3.5 vs 3.9 ms), equalize is unchanged (same VGPR profile)
+  int disp_w2 = 4;
+  int disp_m2 = 1;
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
                     // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)
 };

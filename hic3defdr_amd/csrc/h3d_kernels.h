@@ -570,7 +570,7 @@ static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int 
 }
 
 template <int M>
-__global__ __launch_bounds__(kBrentBlock, 4) void k_brent(
+__global__ __launch_bounds__(kBrentBlock, M >= 16 ? 2 : 4) void k_brent(
     const double* __restrict__ pd, int64_t n,
     const int64_t* __restrict__ seg_start /* D + 1 */, int S, int C,
     const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
@@ -610,9 +610,12 @@ __global__ __launch_bounds__(kBrentBlock, 4) void k_brent(
       // independent chains the scheduler interleaves (the NLL is bound by
       // FP64 dependency latency at 4 waves/SIMD); the terms still join the
       // sum in pixel order
-      for (int64_t px = b + threadIdx.x; px < e; px += 2 * kBrentBlock) {
+      // (M >= 8: one pixel per trip -- the pair spilled at the 128-VGPR
+      // budget of __launch_bounds__(512, 4))
+      constexpr int kPair = M <= 4 ? 2 : 1;
+      for (int64_t px = b + threadIdx.x; px < e; px += kPair * kBrentBlock) {
         const int64_t qx = px + kBrentBlock;
-        const bool two = qx < e;
+        const bool two = kPair == 2 && qx < e;
         double v[M], w[M];
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -620,9 +623,11 @@ __global__ __launch_bounds__(kBrentBlock, 4) void k_brent(
           w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
         }
         const double t0 = nll_pixel<M>(v, nr, kc);
-        const double t1 = nll_pixel<M>(w, nr, kc);
         acc += t0;
-        if (two) acc += t1;
+        if constexpr (kPair == 2) {
+          const double t1 = nll_pixel<M>(w, nr, kc);
+          if (two) acc += t1;
+        }
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
