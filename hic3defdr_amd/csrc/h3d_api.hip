@@ -379,39 +379,12 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     while ((1 << end_bit) <= D) ++end_bit;
     size_t tmp_bytes = 0;
     if (ctx->disp_sort == 2) {
-      // one (distance, max, min count) order per condition. Condition 0's
-      // order gathers the whole AoS rows (vectorised k_gather_soa): its own
-      // replicates straight into raw_s / f_s, the others into a staging
-      // copy; every further condition then re-sorts its staged rows inside
-      // the segments (keys read coalesced) into raw_s / f_s (k_permute_rows).
+      // one (distance, max, min count) order per condition: per condition a
+      // key pass over its replicates' counts, a radix sort, and a tiled
+      // gather of just those replicates' row slices (k_gather_cond_tile)
       idx_out = (int32_t*)scratch(ctx, "idx_out_c", (size_t)n * 4);
-      int32_t* perm2 = (int32_t*)scratch(ctx, "idx_perm2", (size_t)n * 4);
       int32_t* d_reps = (int32_t*)scratch(ctx, "sort_reps", (size_t)C * kMaxReps * 4);
-      const int n_stage = R - nrep[0];  // replicates of conditions >= 1
-      int32_t* t_raw = n_stage ? (int32_t*)scratch(ctx, "perm_raw", (size_t)n * n_stage * 4) : nullptr;
-      double* t_f = n_stage ? (double*)scratch(ctx, "perm_f", (size_t)n * n_stage * 8) : nullptr;
-      if (!idx_out || !perm2 || !d_reps || (n_stage && (!t_raw || !t_f)))
-        return fail(H3D_ENOMEM, "sort buffers");
-      // staging slot of every replicate of conditions >= 1, condition by
-      // condition in design order (so condition c's rows are contiguous)
-      SoaRows rows;
-      std::vector<int> stage_base(C, 0);
-      {
-        int slot = 0;
-        for (int c = 1; c < C; ++c) {
-          stage_base[c] = slot;
-          for (int j = 0; j < nrep[c]; ++j, ++slot) {
-            const int r = rep_idx[(size_t)c * kMaxReps + j];
-            rows.raw[r] = t_raw + (size_t)slot * n;
-            rows.f[r] = t_f + (size_t)slot * n;
-          }
-        }
-        for (int j = 0; j < nrep[0]; ++j) {
-          const int r = rep_idx[j];
-          rows.raw[r] = raw_s + (size_t)r * n;
-          rows.f[r] = f_s + (size_t)r * n;
-        }
-      }
+      if (!idx_out || !d_reps) return fail(H3D_ENOMEM, "sort buffers");
       HIP_TRY(hipMemcpyAsync(d_reps, rep_idx.data(), (size_t)C * kMaxReps * 4,
                              hipMemcpyHostToDevice, s));
       const bool k32 = end_bit <= 16;
@@ -420,53 +393,48 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       void* keys_s = scratch(ctx, "dkeys_s", n * (k32 ? 4 : 8));
       if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
       for (int c = 0; c < C; ++c) {
-        // c = 0: keys of the AoS input, perm into it; c >= 1: keys of the
-        // staged SoA rows (condition 0's order), perm within the segments
-        int32_t* perm = c == 0 ? idx_out : perm2;
-        const int32_t* kdist = c == 0 ? d_dist : dist_s;
-        const int32_t* kraw = c == 0 ? d_raw : t_raw + (size_t)stage_base[c] * n;
+        const int32_t* reps_c = d_reps + c * kMaxReps;
         if (k32) {
           hipLaunchKernelGGL(k_dist_cond_keys<uint32_t>, dim3(grid_for(ctx, n)),
-                             dim3(kBlock), 0, s, kdist, kraw, n, R,
-                             d_reps + c * kMaxReps, nrep[c], cbits, c > 0 ? 1 : 0,
-                             (uint32_t*)keys);
+                             dim3(kBlock), 0, s, d_dist, d_raw, n, R, reps_c, nrep[c],
+                             cbits, (uint32_t*)keys);
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)keys,
-                                                     (uint32_t*)keys_s, idx_in, perm,
+                                                     (uint32_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, 32, s));
           void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
           if (!tmp) return fail(H3D_ENOMEM, "sort temp");
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)keys,
-                                                     (uint32_t*)keys_s, idx_in, perm,
+                                                     (uint32_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, 32, s));
           if (c == 0)
             hipLaunchKernelGGL(k_key_dist<uint32_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
                                0, s, (const uint32_t*)keys_s, n, cbits, dist_s);
         } else {
           hipLaunchKernelGGL(k_dist_cond_keys<uint64_t>, dim3(grid_for(ctx, n)),
-                             dim3(kBlock), 0, s, kdist, kraw, n, R,
-                             d_reps + c * kMaxReps, nrep[c], cbits, c > 0 ? 1 : 0,
-                             (uint64_t*)keys);
+                             dim3(kBlock), 0, s, d_dist, d_raw, n, R, reps_c, nrep[c],
+                             cbits, (uint64_t*)keys);
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint64_t*)keys,
-                                                     (uint64_t*)keys_s, idx_in, perm,
+                                                     (uint64_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, 64, s));
           void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
           if (!tmp) return fail(H3D_ENOMEM, "sort temp");
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint64_t*)keys,
-                                                     (uint64_t*)keys_s, idx_in, perm,
+                                                     (uint64_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, 64, s));
           if (c == 0)
             hipLaunchKernelGGL(k_key_dist<uint64_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
                                0, s, (const uint64_t*)keys_s, n, cbits, dist_s);
         }
-        if (c == 0) {
-          hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                             idx_out, d_raw, d_f, n, R, rows);
-        } else {
-          hipLaunchKernelGGL(k_permute_rows, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                             perm2, t_raw + (size_t)stage_base[c] * n,
-                             t_f + (size_t)stage_base[c] * n, d_reps + c * kMaxReps,
-                             nrep[c], n, raw_s, f_s);
+        SoaRows rows;
+        for (int j = 0; j < nrep[c]; ++j) {
+          const int r = rep_idx[(size_t)c * kMaxReps + j];
+          rows.raw[j] = raw_s + (size_t)r * n;
+          rows.f[j] = f_s + (size_t)r * n;
         }
+        const int64_t tiles = (n + kGatherTile - 1) / kGatherTile;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)ctx->n_cu * 8));
+        hipLaunchKernelGGL(k_gather_cond_tile, dim3(grid), dim3(256), 0, s, idx_out, d_raw,
+                           d_f, n, R, reps_c, nrep[c], rows);
       }
     } else if (ctx->disp_sort == 1 && end_bit <= 16) {
       // (distance, total count) keys: same segments, less lane divergence;

@@ -109,26 +109,53 @@ static __global__ void k_gather_soa(const int32_t* __restrict__ perm,
   }
 }
 
-// one condition's SoA rows re-ordered inside their distance segments:
-// raw_s[reps[j]][i] = src_raw[j][perm[i]] (perm maps within segments, so the
-// reads stay inside a segment's window -- L2-resident, unlike a second random
-// gather of the AoS rows). One pixel order PER CONDITION is sound because
-// every consumer of a condition's SoA rows (equalize, the NLL, the segment
-// sums) touches only that condition's replicates, and all orders share the
-// same distance segments.
-static __global__ void k_permute_rows(const int32_t* __restrict__ perm,
-                                      const int32_t* __restrict__ src_raw,
-                                      const double* __restrict__ src_f,
-                                      const int32_t* __restrict__ reps, int nr, int64_t n,
-                                      int32_t* __restrict__ raw_s,
-                                      double* __restrict__ f_s) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t src = perm[i];
-    for (int j = 0; j < nr; ++j) {
-      raw_s[(int64_t)reps[j] * n + i] = src_raw[(int64_t)j * n + src];
-      f_s[(int64_t)reps[j] * n + i] = src_f[(int64_t)j * n + src];
+// Gather of ONE condition's replicates through that condition's own pixel
+// order: dst row j (replicate reps[j]) = raw / f column reps[j] of the AoS
+// rows perm[i]. A workgroup takes kGatherTile output pixels, reads their
+// row slices cooperatively (consecutive lanes walk along a row, so a wave's
+// load covers whole row slices instead of 64 scattered words), transposes
+// them through LDS and writes each replicate's run of the tile coalesced.
+// One pixel order PER CONDITION is sound because every consumer of a
+// condition's SoA rows (equalize, the NLL, the segment sums) touches only
+// that condition's replicates, and all the orders share the distance
+// segments.
+constexpr int kGatherTile = 128;
+
+static __global__ __launch_bounds__(256) void k_gather_cond_tile(
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ raw,
+    const double* __restrict__ f, int64_t n, int R, const int32_t* __restrict__ reps,
+    int nr, SoaRows dst) {
+  constexpr int TP = kGatherTile, LD = kGatherTile + 1;  // +1: bank spread
+  __shared__ int64_t s_src[TP];
+  __shared__ int s_rep[kMaxReps];
+  __shared__ double s_buf[kMaxReps * LD];
+  int32_t* s_ibuf = reinterpret_cast<int32_t*>(s_buf);
+  if (threadIdx.x < nr) s_rep[threadIdx.x] = reps[threadIdx.x];
+  for (int64_t t0 = (int64_t)blockIdx.x * TP; t0 < n; t0 += (int64_t)gridDim.x * TP) {
+    const int np = (int)((n - t0) < TP ? (n - t0) : TP);
+    if (threadIdx.x < np) s_src[threadIdx.x] = perm[t0 + threadIdx.x];
+    __syncthreads();
+    const int tot = np * nr;
+    for (int q = threadIdx.x; q < tot; q += blockDim.x) {
+      const int p = q / nr, j = q - p * nr;
+      s_ibuf[j * LD + p] = raw[s_src[p] * R + s_rep[j]];
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < nr * TP; q += blockDim.x) {
+      const int j = q / TP, p = q - j * TP;
+      if (p < np) dst.raw[j][t0 + p] = s_ibuf[j * LD + p];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < tot; q += blockDim.x) {
+      const int p = q / nr, j = q - p * nr;
+      s_buf[j * LD + p] = f[s_src[p] * R + s_rep[j]];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < nr * TP; q += blockDim.x) {
+      const int j = q / TP, p = q - j * TP;
+      if (p < np) dst.f[j][t0 + p] = s_buf[j * LD + p];
+    }
+    __syncthreads();
   }
 }
 
@@ -136,14 +163,11 @@ static __global__ void k_permute_rows(const int32_t* __restrict__ perm,
 // condition's replicates; each capped to its half of the cbits count bits).
 // Modelled on the cfg2 census (tools/order_experiment.py): wave lane
 // utilisation of the equalize pass 0.68 with the total-count key -> 0.79.
-// soa = 0: raw is the AoS (n, R) input (replicates reps[0..nr)); soa = 1: raw
-// is the condition's nr consecutive SoA rows [j][i] in an earlier order, dist
-// the matching distances -- coalesced reads.
 template <typename K>
 __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
                                  const int32_t* __restrict__ raw, int64_t n, int R,
                                  const int32_t* __restrict__ reps, int nr, int cbits,
-                                 int soa, K* __restrict__ keys) {
+                                 K* __restrict__ keys) {
   const int lo = cbits / 2, hi = cbits - lo;
   const uint64_t cap_lo = (1ull << lo) - 1ull, cap_hi = (1ull << hi) - 1ull;
   const uint64_t dcap = (uint64_t)(K)~(K)0 >> cbits;
@@ -151,7 +175,7 @@ __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
        i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t mx = 0, mn = ~0ull;
     for (int j = 0; j < nr; ++j) {
-      const uint64_t v = (uint32_t)(soa ? raw[(int64_t)j * n + i] : raw[i * R + reps[j]]);
+      const uint64_t v = (uint32_t)raw[i * R + reps[j]];
       mx = v > mx ? v : mx;
       mn = v < mn ? v : mn;
     }

@@ -16,14 +16,14 @@ def test_pmc_summary_matches_default_workload():
     d = json.load(open(bench.PMC_SUMMARY))
     assert (d['bins'], d['dmax']) == (20000, 250)
     names = [k.split('[')[0] for k in d['kernels']]
-    for kern in ('k_disp_work<4, 4, 0, false>', 'k_brent<4>', 'k_lrt<4, 2>'):
+    for kern in ('k_disp_work<2, 4, 0, false>', 'k_brent<2>', 'k_lrt<4, 2>'):
         assert any(kern in k for k in names), kern
 
 
 def test_pmc_kernel_per_launch():
     d = json.load(open(bench.PMC_SUMMARY))
-    t = bench.pmc_kernel('k_disp_work<4, 4, 0, false>', 20000, 250)
-    es = [v for k, v in d['kernels'].items() if 'k_disp_work<4, 4, 0, false>' in k]
+    t = bench.pmc_kernel('k_disp_work<2, 4, 0, false>', 20000, 250)
+    es = [v for k, v in d['kernels'].items() if 'k_disp_work<2, 4, 0, false>' in k]
     n = sum(e['dispatches'] for e in es)
     want = sum(e['hbm_read_bytes_corrected'] + e['hbm_write_bytes']
                for e in es) / n
@@ -34,7 +34,7 @@ def test_pmc_kernel_per_launch():
     assert abs(t['f64_flops'] - fl) <= 1e-9 * fl and fl > 0
     assert 0 < t['lane_util'] <= 1
     # other workloads were not profiled: the counter figures stay null
-    assert bench.pmc_kernel('k_disp_work<4, 4, 0, false>', 1000, 250) is None
+    assert bench.pmc_kernel('k_disp_work<2, 4, 0, false>', 1000, 250) is None
     assert bench.pmc_kernel('no_such_kernel', 20000, 250) is None
     r = bench.fp64_roof(t, 1e-3)
     assert abs(r['frac'] - t['f64_flops'] / 1e-3 / 1e12 / 78.6) < 1e-12
