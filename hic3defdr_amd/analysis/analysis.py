@@ -22,6 +22,7 @@ chromosomes LPT assigns it for prepare_data and lrt, estimate_disp pools
 the distances genome-wide through a per-pass all-reduce of the NLL sums,
 and BH gathers the p-values on rank 0 and scatters the q-values back.
 """
+import concurrent.futures
 import os
 
 import numpy as np
@@ -44,6 +45,16 @@ def _canonical_csr(fname):
     m = sparse.load_npz(fname).tocsr()
     m.sum_duplicates()  # sorted, duplicate-free rows (what the kernels expect)
     return m
+
+
+def _pixel_factors(bias, row, col, size_factors):
+    """bias[row] * bias[col] * size_factors (analysis.py:181, :272-275), the
+    same products in the same order, through np.take and in-place multiplies
+    (half the time of the fancy-indexed expression's temporaries)."""
+    f = np.take(bias, row, axis=0)
+    f *= np.take(bias, col, axis=0)
+    f *= size_factors
+    return f
 
 
 class AnalyzingHiC3DeFDR(object):
@@ -85,8 +96,13 @@ class AnalyzingHiC3DeFDR(object):
                 'norm=%r: the GPU path implements %s' % (norm, NATIVE_NORMS))
         eprint('preparing data for chrom %s' % chrom, skip=not verbose)
         bias = self.load_bias(chrom)
-        mats = [_canonical_csr(p.replace('<chrom>', chrom))
-                for p in self.raw_npz_patterns]
+        # the replicates' NPZ files decompress concurrently (zlib inflate and
+        # crc32 release the GIL)
+        with concurrent.futures.ThreadPoolExecutor(
+                min(8, len(self.raw_npz_patterns))) as ex:
+            mats = list(ex.map(_canonical_csr,
+                               [p.replace('<chrom>', chrom)
+                                for p in self.raw_npz_patterns]))
         ctx = self._ctx()
         eprint('  computing union pixel set', skip=not verbose)
         row, col, raw, balanced = ctx.sparse_union(mats, bias,
@@ -134,7 +150,7 @@ class AnalyzingHiC3DeFDR(object):
             # (analysis.py:181) and raises IndexError.
             if sf.ndim == 2:
                 sf = sf[di]
-            fs.append(bias[row, :] * bias[col, :] * sf)
+            fs.append(_pixel_factors(bias, row, col, sf))
             dists.append(col - row)
         R = self.design.shape[0]
         offsets = np.concatenate([[0], np.cumsum([len(r) for r in raws])])
@@ -241,9 +257,9 @@ class AnalyzingHiC3DeFDR(object):
         raw = self.load_data('raw', chrom, idx=disp_idx)
         disp = self.load_data('disp', chrom)
         if len(size_factors.shape) == 2:
-            f = bias[row] * bias[col] * size_factors[disp_idx, :]
+            f = _pixel_factors(bias, row, col, size_factors[disp_idx, :])
         else:
-            f = bias[row] * bias[col] * size_factors
+            f = _pixel_factors(bias, row, col, size_factors)
         p, llr, mu0, mu1, _ = self._ctx().lrt(raw, f, None, disp,
                                               self._cond_of_rep(),
                                               refit_mu=refit_mu,

@@ -1,6 +1,7 @@
 """Persistence mixin (reference hic3defdr/analysis/core.py): the outdir is the
 contract between stages — ``<outdir>/<name>_<chrom>.npy`` per chromosome,
 ``disp_per_dist.npy``, ``disp_fn_<cond>.pickle`` and ``pickle``."""
+import os
 import pickle
 
 import numpy as np
@@ -119,14 +120,52 @@ class CoreHiC3DeFDR(object):
         out[np.flatnonzero(mask)[sub]] = True
         return out
 
+    # Write-through cache of the outdir arrays this object saved: a later
+    # stage reading its own output back skips the disk read -- but only while
+    # the file on disk is still the one written (same inode, size and mtime),
+    # so edits or replacements of the outdir files are always seen.
+    def _cache(self):
+        c = self.__dict__.get('_npy_cache')
+        if c is None:
+            c = self.__dict__['_npy_cache'] = {}
+        return c
+
     @staticmethod
-    def _read(fname, idx, col):
+    def _stamp(fname):
+        st = os.stat(fname)
+        return (st.st_ino, st.st_size, st.st_mtime_ns)
+
+    def _cached(self, fname):
+        hit = self._cache().get(fname)
+        if hit is None:
+            return None
+        try:
+            if self._stamp(fname) == hit[0]:
+                return hit[1]
+        except OSError:
+            pass
+        del self._cache()[fname]
+        return None
+
+    def _read(self, fname, idx, col):
         """One .npy, optionally subset by a row mask and/or one column."""
+        a = self._cached(fname)
+        if a is not None:
+            # copies, as np.load hands out fresh arrays
+            if idx is None:
+                return a.copy() if col is None else a[:, col].copy()
+            return a[idx] if col is None else a[idx, col]
         if idx is None:
             a = np.load(fname)
             return a if col is None else a[:, col]
         a = np.load(fname, mmap_mode='r')
         return np.asarray(a[idx] if col is None else a[idx, col])
+
+    def _save_npy(self, fname, data):
+        data = np.asanyarray(data)
+        np.save(fname, data)
+        if type(data) is np.ndarray:
+            self._cache()[fname] = (self._stamp(fname), data.copy())
 
     def load_data(self, name, chrom=None, idx=None, rep=None, cond=None,
                   coo=False):
@@ -172,7 +211,8 @@ class CoreHiC3DeFDR(object):
             fname = self._npy(name, c)
             sub = None
             if idx is not None:
-                n = np.load(fname, mmap_mode='r').shape[0]
+                a = self._cached(fname)
+                n = (a if a is not None else np.load(fname, mmap_mode='r')).shape[0]
                 sub, start = idx[start:start + n], start + n
             pieces.append(self._read(fname, sub, col))
         offsets = np.concatenate([[0], np.cumsum([len(a) for a in pieces])])
@@ -184,9 +224,9 @@ class CoreHiC3DeFDR(object):
         ``self.chroms``."""
         if isinstance(chrom, np.ndarray):
             for c, lo, hi in zip(self.chroms, chrom[:-1], chrom[1:]):
-                np.save(self._npy(name, c), data[lo:hi])
+                self._save_npy(self._npy(name, c), data[lo:hi])
             return
-        np.save(self._npy(name, chrom), data)
+        self._save_npy(self._npy(name, chrom), data)
 
     def load_disp_fn(self, cond):
         """Reference ``core.py:220-236``."""

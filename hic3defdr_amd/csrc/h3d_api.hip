@@ -567,7 +567,13 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                      d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
   if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 16, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
-  const int mslot = (maxnr <= 2 && ctx->disp_m2) ? 2 : maxnr <= 4 ? 4 : maxnr <= 8 ? 8 : maxnr <= 16 ? 16 : 32;
+  // (an M = 6 instantiation for cfg4's R_c = 6 measured equal to M = 8:
+  // 111.5 vs 110.5 ms equalize per step, profiles/r02/q2)
+  const int mslot = (maxnr <= 2 && ctx->disp_m2) ? 2
+                    : maxnr <= 4                  ? 4
+                    : maxnr <= 8                  ? 8
+                    : maxnr <= 16                 ? 16
+                                                  : 32;
   int rounds = 0, batch = 2, rc = 0;
   if (!reduce) {
     // Single rank: one equalize pass per qcml iteration over every segment

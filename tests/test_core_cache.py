@@ -1,0 +1,62 @@
+"""The outdir write-through cache of save_data / load_data (CPU only): a
+stage reading its own output back gets the saved values, fresh arrays every
+time, and any change of the file on disk wins over the cache."""
+import os
+import tempfile
+import time
+
+import numpy as np
+import pandas as pd
+
+from hic3defdr_amd import HiC3DeFDR
+
+
+def _h():
+    out = tempfile.mkdtemp(prefix='h3d_cache_')
+    design = pd.DataFrame([[True, False], [True, False], [False, True]],
+                          index=['a1', 'a2', 'b1'], columns=['A', 'B'])
+    return HiC3DeFDR(['x_<chrom>.npz'] * 3, ['x_<chrom>.bias'] * 3,
+                     ['chr1', 'chr2'], design, out)
+
+
+def test_roundtrip_and_fresh_arrays():
+    h = _h()
+    a = np.arange(12.0).reshape(6, 2)
+    h.save_data(a, 'scaled', 'chr1')
+    a[0, 0] = -1.0                       # the cache holds its own copy
+    b = h.load_data('scaled', 'chr1')
+    assert b[0, 0] == 0.0
+    b[1, 1] = 99.0                       # callers may mutate what they get
+    np.testing.assert_array_equal(h.load_data('scaled', 'chr1'),
+                                  np.arange(12.0).reshape(6, 2))
+    idx = np.array([True, False, True, False, False, True])
+    np.testing.assert_array_equal(h.load_data('scaled', 'chr1', idx=idx),
+                                  np.arange(12.0).reshape(6, 2)[idx])
+    np.testing.assert_array_equal(h.load_data('scaled', 'chr1', cond='B'),
+                                  np.arange(12.0).reshape(6, 2)[:, 1])
+
+
+def test_file_changed_on_disk_wins():
+    h = _h()
+    h.save_data(np.zeros(5), 'disp_idx', 'chr1')
+    fname = os.path.join(h.outdir, 'disp_idx_chr1.npy')
+    time.sleep(0.01)
+    np.save(fname, np.ones(7))           # replaced behind the object's back
+    np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'), np.ones(7))
+    os.remove(fname)
+    np.save(fname, np.full(5, 2.0))      # new inode, same size
+    np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'),
+                                  np.full(5, 2.0))
+
+
+def test_all_chroms_with_offsets_and_idx():
+    h = _h()
+    x = np.arange(10.0)
+    off = np.array([0, 4, 10])
+    h.save_data(x, 'pvalues', off)
+    got, offsets = h.load_data('pvalues', 'all')
+    np.testing.assert_array_equal(got, x)
+    np.testing.assert_array_equal(offsets, off)
+    idx = x % 3 == 0
+    got, offsets = h.load_data('pvalues', 'all', idx=idx)
+    np.testing.assert_array_equal(got, x[idx])

@@ -1,0 +1,42 @@
+"""cProfile of the product's run_to_qvalues on bench.py's cfg2 workload files
+(where the end-to-end wall time goes: NPZ parse, GPU stages, host glue,
+.npy writes). Runs on the GPU box.
+
+    python tools/e2e_profile.py [--bins 20000] [--dmax 250] [--top 30]
+"""
+import argparse
+import cProfile
+import os
+import pstats
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--bins', type=int, default=20000)
+    ap.add_argument('--dmax', type=int, default=250)
+    ap.add_argument('--top', type=int, default=30)
+    args = ap.parse_args()
+    import bench
+    tmp = tempfile.mkdtemp(prefix='h3d_e2eprof_')
+    h, _ = bench.make_workload(tmp, 'chrB', args.bins, args.dmax, seed=0)
+    print('warm-up (first-call costs: library load, HIP init)', flush=True)
+    bench.e2e_wall(h, tmp)
+    prof = cProfile.Profile()
+    t0 = time.perf_counter()
+    prof.enable()
+    stages = bench.e2e_wall(h, tmp)
+    prof.disable()
+    print('stages', stages, 'profiled wall %.3f s' % (time.perf_counter() - t0))
+    st = pstats.Stats(prof)
+    st.sort_stats('cumulative').print_stats(args.top)
+    st.sort_stats('tottime').print_stats(args.top)
+
+
+if __name__ == '__main__':
+    main()
