@@ -153,6 +153,26 @@ H3D_HD double recip_nll(double y) {
 #endif
 }
 
+// Horner step p x + c of the NLL polynomials. On gfx950 an explicit
+// three-address v_fma_f64 with the constant addend in an SGPR pair: with the
+// constant as the tied accumulator the compiler emitted v_fmac_f64 plus a
+// v_mov_b64 copy of the constant per step (84 of the 410 VALU instructions of
+// k_brent's loop). Measured (tools/ab_lib.sh, cfg2): k_brent 3.57 -> 3.07 ms
+// per step; with a VGPR constraint on c the compiler copied the constants
+// from SGPRs instead (3.29 ms). The result is the same fused value the
+// contracted `p * x + c` gave. Operands here never come straight from a
+// transcendental instruction (s^2, r^2, a Horner value), so the asm needs no
+// forwarding wait state. Host: `p * x + c` as before.
+H3D_HD double hfma(double p, double x, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(p), "v"(x), "s"(c));
+  return r;
+#else
+  return p * x + c;
+#endif
+}
+
 // Natural log for finite x > 0 in straight-line code: x = m 2^e with
 // m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh(s), s = (m - 1) / (m + 1),
 // |s| <= 0.1716, by 11 terms of the atanh series (truncation < 1e-18).
@@ -171,18 +191,36 @@ H3D_HD double log_fast(double x) {
   }
   const double s = (m - 1.0) * recip_nll(m + 1.0), s2 = s * s;
   double p = 1.0 / 21.0;
-  p = p * s2 + 1.0 / 19.0;
-  p = p * s2 + 1.0 / 17.0;
-  p = p * s2 + 1.0 / 15.0;
-  p = p * s2 + 1.0 / 13.0;
-  p = p * s2 + 1.0 / 11.0;
-  p = p * s2 + 1.0 / 9.0;
-  p = p * s2 + 1.0 / 7.0;
-  p = p * s2 + 1.0 / 5.0;
-  p = p * s2 + 1.0 / 3.0;
+  p = hfma(p, s2, 1.0 / 19.0);
+  p = hfma(p, s2, 1.0 / 17.0);
+  p = hfma(p, s2, 1.0 / 15.0);
+  p = hfma(p, s2, 1.0 / 13.0);
+  p = hfma(p, s2, 1.0 / 11.0);
+  p = hfma(p, s2, 1.0 / 9.0);
+  p = hfma(p, s2, 1.0 / 7.0);
+  p = hfma(p, s2, 1.0 / 5.0);
+  p = hfma(p, s2, 1.0 / 3.0);
   const double lnm = 2.0 * s + 2.0 * s * s2 * p;
   const double de = (double)e;
   return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + lnm);
+}
+
+// Stirling series of the NLL lgamma in r2 = 1/y^2 (8 Bernoulli terms),
+// Horner from the innermost term: the same fused steps as the nested form
+H3D_HD double stirling_nll(double r2) {
+  double q = -3617.0 / 122400.0;
+  q = hfma(q, r2, 1.0 / 156.0);
+  q = hfma(q, r2, -691.0 / 360360.0);
+  q = hfma(q, r2, 1.0 / 1188.0);
+  q = hfma(q, r2, -1.0 / 1680.0);
+  q = hfma(q, r2, 1.0 / 1260.0);
+  q = hfma(q, r2, -1.0 / 360.0);
+  return hfma(q, r2, 1.0 / 12.0);
+}
+
+// degree-5 rising factorial x (x+1) (x+2) (x+3) (x+4)
+H3D_HD double rise5(double x) {
+  return hfma(hfma(hfma(x + 10.0, x, 35.0), x, 50.0), x, 24.0) * x;
 }
 
 // log Gamma(x), x > 0 finite, for the NLL sums (dispersion.py:67-70), where
@@ -212,21 +250,13 @@ H3D_HD double lgam_nll(double x) {
   if (x < 10.0) {
     const bool two = x < 5.0;
     const double u = two ? x + 5.0 : x;
-    const double pu = ((((u + 10.0) * u + 35.0) * u + 50.0) * u + 24.0) * u;
-    const double px = ((((x + 10.0) * x + 35.0) * x + 50.0) * x + 24.0) * x;
+    const double pu = rise5(u);
+    const double px = rise5(x);
     P = two ? px * pu : pu;
     y = u + 5.0;
   }
   const double r = recip_nll(y), r2 = r * r;
-  const double corr =
-      r * (1.0 / 12.0 +
-           r2 * (-1.0 / 360.0 +
-                 r2 * (1.0 / 1260.0 +
-                       r2 * (-1.0 / 1680.0 +
-                             r2 * (1.0 / 1188.0 +
-                                   r2 * (-691.0 / 360360.0 +
-                                         r2 * (1.0 / 156.0 +
-                                               r2 * (-3617.0 / 122400.0))))))));
+  const double corr = r * stirling_nll(r2);
   double v = (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
   if (x < 10.0) v -= log_fast(P);
   return v;
@@ -244,22 +274,14 @@ H3D_HD double lgam_nll_parts(double x, double* P) {
   if (x < 10.0) {
     const bool two = x < 5.0;
     const double u = two ? x + 5.0 : x;
-    const double pu = ((((u + 10.0) * u + 35.0) * u + 50.0) * u + 24.0) * u;
-    const double px = ((((x + 10.0) * x + 35.0) * x + 50.0) * x + 24.0) * x;
+    const double pu = rise5(u);
+    const double px = rise5(x);
     p = two ? px * pu : pu;
     y = u + 5.0;
   }
   *P = p;
   const double r = recip_nll(y), r2 = r * r;
-  const double corr =
-      r * (1.0 / 12.0 +
-           r2 * (-1.0 / 360.0 +
-                 r2 * (1.0 / 1260.0 +
-                       r2 * (-1.0 / 1680.0 +
-                             r2 * (1.0 / 1188.0 +
-                                   r2 * (-691.0 / 360360.0 +
-                                         r2 * (1.0 / 156.0 +
-                                               r2 * (-3617.0 / 122400.0))))))));
+  const double corr = r * stirling_nll(r2);
   return (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
 }
 
@@ -351,7 +373,14 @@ H3D_HD double igam_series_sum(double a, double x) {
   for (int i = 0; i < kMaxIter / 2; ++i) {
     H3D_STAT(ser_it, 2);
     const double r1 = r + 1.0, r2 = r + 2.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // gfx950: v_rcp_f64 + one Newton step (~1 ulp) instead of the IEEE
+    // division sequence (10 FP64 instructions, 40% of the trip); the terms
+    // then carry ~1 ulp more rounding each, far below the sum's own error
+    const double xi = x * recip_nll(r1 * r2);
+#else
     const double xi = x / (r1 * r2);
+#endif
     c *= xi * r2;
     ans += c;
     if (c <= kMachEp * ans) break;
@@ -398,6 +427,12 @@ H3D_HD double igamc_series(double a, double x) {
 // and the quotient is formed once at the end. tol = 4 eps: the fused
 // cross product is exact to ~1 eps of |p_k q_{k-1}|, so the test is met once
 // the convergents agree to ~3 eps (cephes: once they round to the same double).
+// The overflow guard rescales all four convergent terms by 2^-52 once per
+// trip (two steps), branch-free (a multiply by 1 or 2^-52): scaling by a
+// power of two changes neither the test nor the final quotient, so the result
+// is bit-identical to a per-step guard, and the loop body carries no masked
+// copy-and-scale region (on gfx950 that region cost 4 v_mov_b64 + 4 v_ldexp
+// + exec-mask updates per step, a third of the step).
 H3D_HD double igamc_cf_ratio(double a, double x) {
 #if defined(__clang__)
   // contraction (the convergents' products fuse into FMAs) -- the ratio
@@ -418,12 +453,6 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
     q0 = q1 * z - q0 * yc;
     double lead = p0 * q1;
     bool done = (q0 != 0.0) && fabs(lead - p1 * q0) <= 4.0 * kMachEp * fabs(lead);
-    if (fabs(p0) > kBig) {
-      p0 *= kBigInv;
-      q0 *= kBigInv;
-      p1 *= kBigInv;
-      q1 *= kBigInv;
-    }
     if (done) return p0 / q0;
     H3D_STAT(cf_it, 1);
     c += 1.0;
@@ -434,13 +463,12 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
     q1 = q0 * z - q1 * yc;
     lead = p1 * q0;
     done = (q1 != 0.0) && fabs(lead - p0 * q1) <= 4.0 * kMachEp * fabs(lead);
-    if (fabs(p1) > kBig) {
-      p0 *= kBigInv;
-      q0 *= kBigInv;
-      p1 *= kBigInv;
-      q1 *= kBigInv;
-    }
     if (done) return p1 / q1;
+    const double sc = (fmax(fabs(p0), fabs(p1)) > kBig) ? kBigInv : 1.0;
+    p0 *= sc;
+    q0 *= sc;
+    p1 *= sc;
+    q1 *= sc;
   }
   return p1 / q1;
 }
