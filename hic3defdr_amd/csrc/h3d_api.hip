@@ -198,6 +198,7 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
                   SegState* st, const int* seg_flags, double* result, int* queue) {
   ProfScope ps(ctx, "disp_nll", 0);
   auto k = k_brent<M>;
+  constexpr int kBrentBlock = brent_block<M>();
   int& nb = ctx->resident[(const void*)k];
   if (nb == 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBrentBlock, 0) != hipSuccess ||

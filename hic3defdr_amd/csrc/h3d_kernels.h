@@ -23,7 +23,15 @@ namespace h3d {
 constexpr int kChunk = 256;  // pixels per disp work item (= block size)
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / 64;  // disp partials per work item
-constexpr int kBrentBlock = 512;  // k_brent: one workgroup per segment
+// k_brent: one workgroup per segment. 1024 threads: a cfg2 step has ~500
+// segments, so the workgroup count, not the register budget, set the waves
+// per SIMD; measured (tools/ab_lib.sh) k_brent<2> 3.34 -> 2.95 ms per step
+// against 512 (768: 3.25). M >= 16 keeps 512 threads: its loop needs more
+// than the 128 VGPRs a 1024-thread workgroup leaves a lane.
+template <int M>
+constexpr int brent_block() {
+  return M >= 16 ? 512 : 1024;
+}
 
 // deterministic wave sum (fixed butterfly); result valid in every lane
 __device__ inline double wave_sum(double v) {
@@ -594,7 +602,7 @@ static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int 
 }
 
 template <int M>
-__global__ __launch_bounds__(kBrentBlock, M >= 16 ? 2 : 4) void k_brent(
+__global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     const double* __restrict__ pd, int64_t n,
     const int64_t* __restrict__ seg_start /* D + 1 */, int S, int C,
     const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
@@ -605,6 +613,7 @@ __global__ __launch_bounds__(kBrentBlock, M >= 16 ? 2 : 4) void k_brent(
   // only holds the four NLL constants (the SegState in every thread's VGPRs
   // spilled at the 1024-thread register budget)
   __shared__ SegState s_st;
+  constexpr int kBrentBlock = brent_block<M>();
   __shared__ double wpart[kBrentBlock / 64];
   __shared__ int s_next, s_more;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
