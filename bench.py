@@ -281,6 +281,11 @@ def main():
     ap.add_argument('--cpu-bins', type=int, default=1000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--noop-reduce', action='store_true',
+                    help='measurement: run the multi-rank estimate_disp driver '
+                         '(per-pass NLL sums through the reduce hook) on one '
+                         'GPU with a no-op reduce, i.e. the N > 1 kernel and '
+                         'host-sync path without the collective')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -324,6 +329,9 @@ def main():
         torch.cuda.set_stream(stream)
         ctx.set_stream(stream.cuda_stream)
         reduce = parallel.make_allreduce() if world > 1 else None
+        if args.noop_reduce and world == 1:
+            def reduce(ptr, count):
+                pass
 
         def step():
             dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
@@ -430,7 +438,9 @@ def main():
                                 % (args.bins, args.dmax),
                     'disp_pixels_per_gpu': n, 'disp_pixels_total': tot_px,
                     'parallelism': 'dp%d (chromosome shards; %s)' % (
-                        world, 'in-kernel Brent searches' if world == 1 else
+                        world, 'per-pass NLL sums, no-op reduce (the N > 1 '
+                        'driver on one GPU)' if reduce and world == 1 else
+                        'in-kernel Brent searches' if world == 1 else
                         'per-pass NLL all-reduce over RCCL')},
                 'roofline': roof,
                 'kernel_rooflines': {

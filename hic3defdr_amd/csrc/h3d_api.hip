@@ -157,7 +157,9 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, \
                        st, seg_flags, list, meta, partial);                         \
   } while (0)
-    if constexpr (M == 2) {
+    if constexpr (M == 2 && NLL) {
+      H3D_EQ(4);
+    } else if constexpr (M == 2) {
       // H3D_DISP_W2: the R_c <= 2 path (cfg2's 2 + 2 design)
       if (ctx->disp_w2 == 8) H3D_EQ(8);
       else if (ctx->disp_w2 == 6) H3D_EQ(6);
@@ -625,7 +627,13 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   while (reduce && !rc) {
     for (int b = 0; b < batch; ++b) {
       {
+        // every width the single-rank driver picks (mslot 2 fell through to
+        // the M = 32 instantiation here: 13.1 vs 5.5 ms of equalize per cfg2
+        // step, bench --noop-reduce)
         switch (mslot) {
+          case 2:
+            launch_disp_work<2, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
+            break;
           case 4:
             launch_disp_work<4, true>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C, d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial);
             break;
