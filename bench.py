@@ -328,15 +328,24 @@ def main():
         stream = torch.cuda.Stream(dev)
         torch.cuda.set_stream(stream)
         ctx.set_stream(stream.cuda_stream)
-        reduce = parallel.make_allreduce() if world > 1 else None
+        # N > 1: pixels re-sharded by distance (one all_to_all, single-GPU
+        # driver per rank, one table all-reduce); H3D_DISP_SHARD=pass keeps
+        # them in place and all-reduces the NLL sums of every data pass
+        by_dist = world > 1 and os.environ.get('H3D_DISP_SHARD') != 'pass'
+        reduce = parallel.make_allreduce() if world > 1 and not by_dist \
+            else None
         if args.noop_reduce and world == 1:
             def reduce(ptr, count):
                 pass
 
         def step():
-            dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
-                                        t_dist.data_ptr(), n, R, cond, C, D,
-                                        reduce=reduce)
+            if by_dist:
+                dpd = parallel.disp_per_dist_by_distance(
+                    ctx, t_raw, t_f, t_dist, cond, C, D)
+            else:
+                dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                            t_dist.data_ptr(), n, R, cond, C,
+                                            D, reduce=reduce)
             tab = _native.disp_tables(dpd)
             ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
                         tab, n, R, cond, t_p.data_ptr(), t_llr.data_ptr(),
@@ -441,7 +450,9 @@ def main():
                         world, 'per-pass NLL sums, no-op reduce (the N > 1 '
                         'driver on one GPU)' if reduce and world == 1 else
                         'in-kernel Brent searches' if world == 1 else
-                        'per-pass NLL all-reduce over RCCL')},
+                        'distance re-shard: all_to_all of the disp pixels, '
+                        'in-kernel Brent per rank, table all-reduce' if by_dist
+                        else 'per-pass NLL all-reduce over RCCL')},
                 'roofline': roof,
                 'kernel_rooflines': {
                     'nll_k_brent': {

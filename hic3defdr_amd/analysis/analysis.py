@@ -19,7 +19,8 @@ process pools (util/parallelization.py) are replaced by the GPU. Under
 torchrun (a torch.distributed process group is initialised) every stage
 shards itself over the ranks (hic3defdr_amd.parallel): each rank owns the
 chromosomes LPT assigns it for prepare_data and lrt, estimate_disp pools
-the distances genome-wide through a per-pass all-reduce of the NLL sums,
+the distances genome-wide by re-sharding the disp pixels by distance (one
+all_to_all; every rank then runs the single-GPU driver on its distances),
 and BH gathers the p-values on rank 0 and scatters the q-values back.
 """
 import concurrent.futures
@@ -162,9 +163,11 @@ class AnalyzingHiC3DeFDR(object):
 
     def _disp_per_dist_sharded(self, sh, raw, f, dist, C, D):
         """estimate_disp's per-(distance, condition) qcml over every rank's
-        pixels: this rank's pixels on its GPU, the NLL sums of each data pass
-        all-reduced across ranks (parallel.make_allreduce) on torch's stream,
-        so every rank ends with the same disp_per_dist."""
+        pixels: re-sharded by distance (parallel.disp_per_dist_by_distance:
+        one all_to_all, the single-GPU driver per rank, one all-reduce of the
+        table), or with H3D_DISP_SHARD=pass kept in place with the NLL sums
+        of each data pass all-reduced (parallel.make_allreduce); every rank
+        ends with the same disp_per_dist."""
         import torch
         ctx = self._ctx()
         dev = torch.device('cuda', ctx.device)
@@ -181,6 +184,9 @@ class AnalyzingHiC3DeFDR(object):
         ctx.set_stream(stream.cuda_stream)
         try:
             with torch.cuda.stream(stream):
+                if os.environ.get('H3D_DISP_SHARD') != 'pass':
+                    return parallel.disp_per_dist_by_distance(
+                        ctx, t_raw, t_f, t_d, self._cond_of_rep(), C, D)
                 return ctx.disp_per_dist_dev(
                     t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
                     self.design.shape[0], self._cond_of_rep(), C, D,

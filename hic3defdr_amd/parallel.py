@@ -13,13 +13,20 @@ and scatters the q-values back (``distributed_bh``).
   (``lpt_assign``); no data-path collective.
 * estimate_disp pools every distance genome-wide (reference
   analysis.py:169-206), so per-shard dispersions would NOT equal the
-  reference. Instead every rank keeps its own pixels and the per-(distance,
-  condition) NLL sums of each Brent step are summed across ranks with one
-  small all-reduce (D x C doubles, ~3 KB) per data pass
-  (``make_allreduce``). Every rank then advances identical qcml/Brent state
-  machines, so all ranks finish with the same disp_per_dist, bit for bit,
-  and smooth it identically. The only change from one GPU is the order in
-  which the per-rank partial sums are added (ULP-level).
+  reference. The segments (distance, condition) are independent of each
+  other, so the pixels are re-sharded by DISTANCE for this stage
+  (``disp_per_dist_by_distance``): one all_to_all moves every disp pixel
+  (raw, f, dist: 12 R + 4 bytes) to the rank owning its distance (d mod
+  world), each rank runs the single-GPU driver -- every Brent search
+  in-kernel -- on the distances it owns, and one all-reduce of the D x C
+  table (owners' rows, zeros elsewhere) gives every rank the same
+  disp_per_dist. Two collectives per estimate_disp instead of one per data
+  pass; the only change from one GPU is the order of each segment's pixels
+  (ULP-level).
+* The per-pass alternative (``make_allreduce``, H3D_DISP_SHARD=pass) keeps
+  the pixels in place and all-reduces the per-(distance, condition) NLL sums
+  of every Brent step (D x C doubles, ~3 KB, ~54 passes per cfg2
+  estimate_disp); every rank advances identical state machines.
 """
 import ctypes
 import os
@@ -47,6 +54,63 @@ class _CudaArray(object):
         self.__cuda_array_interface__ = {
             'shape': (int(count),), 'typestr': '<f8',
             'data': (int(ptr), False), 'version': 3, 'strides': None}
+
+
+def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
+                              group=None):
+    """estimate_disp's (D, C) disp_per_dist over every rank's pixels: the
+    pixels move to the rank owning their distance (d mod world) with ONE
+    all_to_all, each rank runs the single-GPU driver on what it received,
+    and ONE all-reduce of the owners' rows gives every rank the whole table.
+
+    t_raw (n, R) int32, t_f (n, R) float64, t_dist (n,) int32: this rank's
+    disp pixels on its GPU. libh3d must run on torch's current stream (a real
+    one: see make_allreduce). Returns the table as a (D, C) numpy array."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = t_raw.device
+    n, R = t_raw.shape
+    owner = t_dist.long() % world
+    order = torch.argsort(owner, stable=True)
+    width = 12 * R + 4
+
+    def as_bytes(t, w):
+        if n == 0:  # an empty tensor's stride cannot be re-viewed
+            return torch.empty((0, w), dtype=torch.uint8, device=dev)
+        return t.contiguous().view(torch.uint8).reshape(n, w)
+
+    # one byte record per pixel: raw (4 R) | f (8 R) | dist (4)
+    rec = torch.cat([as_bytes(t_raw, 4 * R), as_bytes(t_f, 8 * R),
+                     as_bytes(t_dist, 4)], dim=1)[order].contiguous()
+    send = torch.bincount(owner, minlength=world)
+    # gloo exchanges host tensors
+    xdev = dev if dist.get_backend(group) != 'gloo' else torch.device('cpu')
+    recv = torch.empty_like(send, device=xdev)
+    dist.all_to_all_single(recv, send.to(xdev), group=group)
+    s_list, r_list = send.tolist(), recv.tolist()
+    m = int(sum(r_list))
+    out = torch.empty((m, width), dtype=torch.uint8, device=xdev)
+    dist.all_to_all_single(out, rec.to(xdev), output_split_sizes=r_list,
+                           input_split_sizes=s_list, group=group)
+    out = out.to(dev)
+    if m:
+        raw_m = out[:, :4 * R].contiguous().view(torch.int32).reshape(m, R)
+        f_m = out[:, 4 * R:12 * R].contiguous().view(torch.float64).reshape(m, R)
+        dist_m = out[:, 12 * R:].contiguous().view(torch.int32).reshape(m)
+    else:
+        raw_m = torch.empty((0, R), dtype=torch.int32, device=dev)
+        f_m = torch.empty((0, R), dtype=torch.float64, device=dev)
+        dist_m = torch.empty(0, dtype=torch.int32, device=dev)
+    tab = ctx.disp_per_dist_dev(raw_m.data_ptr(), f_m.data_ptr(),
+                                dist_m.data_ptr(), m, R, cond_of_rep, C, D)
+    own = (np.arange(D) % world) == rank
+    tab[~own] = 0.0
+    t_tab = torch.from_numpy(tab).to(xdev)
+    dist.all_reduce(t_tab, op=dist.ReduceOp.SUM, group=group)
+    return t_tab.cpu().numpy()
 
 
 def make_allreduce(group=None):

@@ -1,9 +1,12 @@
 """Multi-rank product on the GPU: HiC3DeFDR.run_to_qvalues() under torchrun
 with 2 ranks on cuda:0 (gloo on device tensors), launched as fresh child
 processes. Every chromosome is prepared and tested by the rank LPT assigns
-it, estimate_disp runs the device driver's multi-rank branch (per-pass
-all-reduce of the NLL sums through parallel.make_allreduce on torch's
-stream), BH gathers on rank 0 and scatters back. The outdir must match the
+it; estimate_disp runs either the distance re-shard (default: one
+all_to_all of the disp pixels, the single-GPU driver per rank, one table
+all-reduce; parallel.disp_per_dist_by_distance) or the device driver's
+multi-rank branch (H3D_DISP_SHARD=pass: per-pass all-reduce of the NLL sums
+through parallel.make_allreduce on torch's stream); BH gathers on rank 0 and
+scatters back. The outdir must match the
 reference goldens like the single-rank run does (tests/test_gpu_e2e.py).
 
 The file sorts first so the pytest process has not touched the GPU when it
@@ -24,15 +27,19 @@ from conftest import REPO, e2e_inputs, rel_err
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize('shard', ['distance', 'pass'])
 @pytest.mark.parametrize('name', ['small2'])
-def test_two_ranks_run_to_qvalues_matches_reference(name):
+def test_two_ranks_run_to_qvalues_matches_reference(name, shard):
     g, kw = e2e_inputs(name)
     assert len(kw['chroms']) == 2   # one chromosome per rank
     outdir = tempfile.mkdtemp(prefix='h3d_dist_')
     try:
         env = dict(os.environ, H3D_DEVICE='0', MASTER_ADDR='127.0.0.1',
                    OMP_NUM_THREADS='1', H3D_DEBUG='1')
-        port = 29600 + os.getpid() % 1000
+        env.pop('H3D_DISP_SHARD', None)
+        if shard == 'pass':
+            env['H3D_DISP_SHARD'] = 'pass'
+        port = 29600 + os.getpid() % 1000 + (7 if shard == 'pass' else 0)
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
                '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
                '--master-port', str(port),

@@ -114,6 +114,78 @@ def test_sharded_disp_equals_single_rank_and_oracle():
         np.testing.assert_allclose(sharded, dpd, rtol=1e-6, atol=1e-12)
 
 
+class _HostCtx(object):
+    """Stands in for the GPU context in disp_per_dist_by_distance on CPU:
+    disp_per_dist_dev reads the received host tensors through their
+    addresses and runs the host emulation of the single-rank driver."""
+
+    def disp_per_dist_dev(self, d_raw, d_f, d_dist, n, R, cond_of_rep, C, Dd,
+                          reduce=None):
+        assert reduce is None and Dd == D
+
+        def arr(ptr, ctype, count):
+            if count == 0:
+                return np.zeros(0, dtype=np.dtype(ctype))
+            buf = (ctype * count).from_address(ptr)
+            return np.frombuffer(buf, dtype=np.dtype(ctype)).copy()
+        raw = arr(d_raw, ctypes.c_int32, n * R).reshape(n, R)
+        f = arr(d_f, ctypes.c_double, n * R).reshape(n, R)
+        dist_ = arr(d_dist, ctypes.c_int32, n)
+        return _rounds(raw, f, dist_, np.asarray(cond_of_rep))
+
+
+def _reshard_worker(rank, world, tmp, port, result_file):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    kw, data = _prep(os.path.join(tmp, 'r%d' % rank))
+    mine = parallel.lpt_assign({c: len(data[c][2]) for c in CHROMS},
+                               world)[rank]
+    R = kw['design'].shape[0]
+    raw = np.concatenate([data[c][2] for c in mine] or
+                         [np.zeros((0, R), np.int32)])
+    f = np.concatenate([data[c][3] for c in mine] or [np.zeros((0, R))])
+    dist_ = np.concatenate([data[c][4] for c in mine] or
+                           [np.zeros(0, np.int32)])
+    cond = kw['design'].argmax(axis=1).astype(np.int32)
+    out = parallel.disp_per_dist_by_distance(
+        _HostCtx(), torch.from_numpy(np.ascontiguousarray(raw, np.int32)),
+        torch.from_numpy(np.ascontiguousarray(f)),
+        torch.from_numpy(np.ascontiguousarray(dist_, np.int32)), cond,
+        kw['design'].shape[1], D)
+    np.save(result_file % rank, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_distance_reshard_equals_single_rank(world):
+    """parallel.disp_per_dist_by_distance: the all_to_all routing by distance
+    (byte records of raw / f / dist), the per-rank single-rank driver and
+    the owners' table all-reduce give every rank the single-process table.
+    world 3 > 2 chromosomes: one rank starts without pixels."""
+    h3dbuild.build_hosttest()
+    with tempfile.TemporaryDirectory() as tmp:
+        res = os.path.join(tmp, 'out_%d.npy')
+        port = 29700 + (os.getpid() % 1000) + world
+        mp.spawn(_reshard_worker, args=(world, tmp, port, res), nprocs=world,
+                 join=True)
+        kw, data = _prep(os.path.join(tmp, 'single'))
+        raw = np.concatenate([data[c][2] for c in CHROMS])
+        f = np.concatenate([data[c][3] for c in CHROMS])
+        dist_ = np.concatenate([data[c][4] for c in CHROMS])
+        single = _rounds(raw, f, dist_, kw['design'].argmax(axis=1))
+        outs = [np.load(res % r) for r in range(world)]
+        for o in outs[1:]:
+            np.testing.assert_array_equal(o, outs[0])
+        np.testing.assert_array_equal(np.isnan(outs[0]), np.isnan(single))
+        # a segment's pixels arrive in rank order, not chromosome order: only
+        # the order of its NLL partial sums differs
+        np.testing.assert_allclose(outs[0], single, rtol=1e-6, atol=1e-12)
+
+
 def _bh_worker(rank, world, port, chroms, pv, result_file):
     """Product orchestration on gloo: Shards (LPT over the chromosomes) and
     the genome-wide BH gather (rank 0) / scatter (parallel.distributed_bh)."""
