@@ -118,14 +118,32 @@ inline std::vector<double> rolling_var_center(const std::vector<double>& v,
   return out;
 }
 
-// statsmodels lowess on x sorted ascending (it robustness iterations)
+// statsmodels lowess on x sorted ascending (it robustness iterations).
+// The control flow (window sliding, delta skipping, copies for equal x,
+// interpolation of skipped points) runs over the points as given; the
+// per-fit sums run over RUNS of equal x instead: every point of a run has the
+// same distance weight and -- as the weighted fit's expanded points are
+// copies of one (x, y) pair -- the same robustness weight, so a run that
+// covers c points of the window contributes c times one term. The weighted
+// lowess_fit replicates each distance floor(weight) times (lowess.py:
+// 186-201), so its fits sum ~k / (mean multiplicity) terms instead of k.
+// Sums are sequential over runs (statsmodels: numpy sums over points): the
+// tables move by rounding only (<= 1e-12 vs the reference, test_abi.py).
 inline std::vector<double> lowess_sorted(const std::vector<double>& x,
                                          const std::vector<double>& y,
                                          double frac, int it, double delta) {
   const int64_t n = (int64_t)x.size();
   int64_t k = (int64_t)(frac * n + 1e-10);
   k = std::min<int64_t>(std::max<int64_t>(k, 2), n);
-  std::vector<double> resid_w(n, 1.0), y_fit(n, 0.0), w(n);
+  // runs of equal (x, y): [rs[r], rs[r + 1]); run_of[point]
+  std::vector<int64_t> rs, run_of(n);
+  for (int64_t i = 0; i < n; ++i) {
+    if (i == 0 || x[i] != x[i - 1] || !(y[i] == y[i - 1])) rs.push_back(i);
+    run_of[i] = (int64_t)rs.size() - 1;
+  }
+  const int64_t nr = (int64_t)rs.size();
+  rs.push_back(n);
+  std::vector<double> run_rw(nr, 1.0), y_fit(n, 0.0);
   for (int rob = 0; rob <= it; ++rob) {
     std::fill(y_fit.begin(), y_fit.end(), 0.0);
     int64_t i = 0, last_fit_i = -1, left = 0, right = k;
@@ -136,34 +154,42 @@ inline std::vector<double> lowess_sorted(const std::vector<double>& x,
         ++right;
       }
       const double radius = std::fmax(xval - x[left], x[right - 1] - xval);
-      const int64_t m = right - left;
-      for (int64_t j = 0; j < m; ++j) {
-        double t = std::fabs(x[left + j] - xval) / radius;
-        double c = t * (t * t);
-        double u = 1 - c;
+      const int64_t r0 = run_of[left], r1 = run_of[right - 1];
+      // One pass of five independent sums over the window's runs, in the
+      // offsets d = x - xval: S0 = sum w, S1 = sum w d, S2 = sum w d^2,
+      // T0 = sum w y, T1 = sum w d y (statsmodels: four dependent passes --
+      // normalise, weighted mean, weighted variance, the hat-matrix row --
+      // whose serial add chains bounded this loop). With mean m = S1 / S0
+      // and var = S2 / S0 - m^2 (the window is within k points of xval, so
+      // |m| stays within a few standard deviations: mild cancellation),
+      //   fit = T0 / S0 - m (T1 / S0 - m T0 / S0) / var,
+      // the same local-linear value up to rounding (tables <= 1e-12 vs the
+      // reference, test_abi.py).
+      const double inv_radius = 1.0 / radius;
+      double S0 = 0.0, S1 = 0.0, S2 = 0.0, T0 = 0.0, T1 = 0.0;
+      for (int64_t r = r0; r <= r1; ++r) {
+        const int64_t a = rs[r];
+        const double c = (double)(std::min(rs[r + 1], right) - std::max(a, left));
+        const double d = x[a] - xval;
+        double t = std::fabs(d) * inv_radius;
+        double u = 1 - t * (t * t);
         u = u > 0.0 ? u : 0.0;
         double wt = u * (u * u);
-        if (rob > 0) wt = wt * resid_w[left + j];
-        w[j] = wt;
+        if (rob > 0) wt = wt * run_rw[r];
+        const double cw = c * wt, cwd = cw * d;
+        S0 += cw;
+        S1 += cwd;
+        S2 += cwd * d;
+        T0 += cw * y[a];
+        T1 += cwd * y[a];
       }
-      const double sw = np_pairwise(w.data(), m);
-      if (sw <= 0.0) {
+      if (S0 <= 0.0) {
         y_fit[i] = y[i];
       } else {
-        for (int64_t j = 0; j < m; ++j) w[j] = w[j] / sw;
-        double swx = 0.0;
-        for (int64_t j = 0; j < m; ++j) swx += w[j] * x[left + j];
-        double sq = 0.0;
-        for (int64_t j = 0; j < m; ++j) {
-          double dv = x[left + j] - swx;
-          sq += w[j] * (dv * dv);
-        }
-        double acc = 0.0;
-        for (int64_t j = 0; j < m; ++j) {
-          double p = w[j] * (1.0 + (xval - swx) * (x[left + j] - swx) / sq);
-          acc += p * y[left + j];
-        }
-        y_fit[i] = acc;
+        const double inv = 1.0 / S0;
+        const double m = S1 * inv, t0 = T0 * inv;
+        const double var = S2 * inv - m * m;
+        y_fit[i] = t0 - m * (T1 * inv - m * t0) / var;
       }
       if (last_fit_i < i - 1) {
         const double den = x[i] - x[last_fit_i];
@@ -193,16 +219,19 @@ inline std::vector<double> lowess_sorted(const std::vector<double>& x,
         ab[j] = std::fabs(res[j]);
       }
       std::vector<double> srt(ab);
-      std::sort(srt.begin(), srt.end());
-      const double med = (n % 2) ? srt[n / 2]
-                                 : 0.5 * (srt[n / 2 - 1] + srt[n / 2]);
+      std::nth_element(srt.begin(), srt.begin() + n / 2, srt.end());
+      double med = srt[n / 2];
+      if (n % 2 == 0)
+        med = 0.5 * (*std::max_element(srt.begin(), srt.begin() + n / 2) + med);
       const double s6 = 6.0 * med;
-      for (int64_t j = 0; j < n; ++j) {
+      // robustness weight per run: its points share y and (equal x) the fit
+      for (int64_t r = 0; r < nr; ++r) {
+        const double rj = res[rs[r]];
         if (s6 > 0) {
-          double t = std::fabs(res[j] / s6);
-          resid_w[j] = (t < 1.0) ? (1 - t * t) * (1 - t * t) : 0.0;
+          double t = std::fabs(rj / s6);
+          run_rw[r] = (t < 1.0) ? (1 - t * t) * (1 - t * t) : 0.0;
         } else {
-          resid_w[j] = (res[j] == 0) ? 1.0 : 0.0;
+          run_rw[r] = (rj == 0) ? 1.0 : 0.0;
         }
       }
     }
