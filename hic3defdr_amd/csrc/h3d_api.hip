@@ -297,6 +297,7 @@ void h3d_close(h3d_ctx* ctx) {
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->work_count) (void)hipFree(ctx->work_count);
   if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -534,21 +535,46 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   for (int d = 0; d < D; ++d)
     for (int c = 0; c < C; ++c) lpx[d * C + c] = seg_start[d + 1] - seg_start[d];
 
-  auto up = [&](const char* slot, const void* src, size_t bytes) -> void* {
-    void* p = scratch(ctx, slot, bytes);
-    if (p && bytes) (void)hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, s);
-    return p;
-  };
-  int64_t* d_cs = (int64_t*)up("chunk_start", cs.data(), cs.size() * 8);
-  int32_t* d_cl = (int32_t*)up("chunk_len", cl.data(), cl.size() * 4);
-  int32_t* d_cd = (int32_t*)up("chunk_d", cd.data(), cd.size() * 4);
-  int32_t* d_scb = (int32_t*)up("seg_chunk_b", scb.data(), D * 4);
-  int32_t* d_sce = (int32_t*)up("seg_chunk_e", sce.data(), D * 4);
+  // the per-call tables go up as ONE copy from a pinned staging buffer (nine
+  // pageable copies cost ~0.3 ms of host-side gaps per cfg2 step: each
+  // staged and launched its own blit)
   std::vector<int32_t> nrep32(nrep.begin(), nrep.end());
-  int32_t* d_nrep = (int32_t*)up("n_rep", nrep32.data(), C * 4);
-  int32_t* d_repidx = (int32_t*)up("rep_idx", rep_idx.data(), rep_idx.size() * 4);
-  SegState* d_st = (SegState*)up("seg_state", st.data(), S * sizeof(SegState));
-  int64_t* d_lpx = (int64_t*)up("seg_px", lpx.data(), S * 8);
+  struct Part {
+    const void* src;
+    size_t bytes, off;
+  };
+  Part parts[] = {{cs.data(), cs.size() * 8, 0},       {cl.data(), cl.size() * 4, 0},
+                  {cd.data(), cd.size() * 4, 0},       {scb.data(), (size_t)D * 4, 0},
+                  {sce.data(), (size_t)D * 4, 0},      {nrep32.data(), (size_t)C * 4, 0},
+                  {rep_idx.data(), rep_idx.size() * 4, 0},
+                  {st.data(), (size_t)S * sizeof(SegState), 0},
+                  {lpx.data(), (size_t)S * 8, 0}};
+  size_t blob = 0;
+  for (Part& q : parts) {
+    q.off = blob;
+    blob += (q.bytes + 255) & ~(size_t)255;
+  }
+  if (ctx->h_stage_bytes < blob) {
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->h_stage_bytes = 0;
+    HIP_TRY(hipHostMalloc(&ctx->h_stage, blob, hipHostMallocDefault));
+    ctx->h_stage_bytes = blob;
+  }
+  char* d_blob = (char*)scratch(ctx, "disp_tables", blob);
+  if (!d_blob) return fail(H3D_ENOMEM, "disp tables");
+  for (const Part& q : parts)
+    if (q.bytes) std::memcpy((char*)ctx->h_stage + q.off, q.src, q.bytes);
+  HIP_TRY(hipMemcpyAsync(d_blob, ctx->h_stage, blob, hipMemcpyHostToDevice, s));
+  int64_t* d_cs = (int64_t*)(d_blob + parts[0].off);
+  int32_t* d_cl = (int32_t*)(d_blob + parts[1].off);
+  int32_t* d_cd = (int32_t*)(d_blob + parts[2].off);
+  int32_t* d_scb = (int32_t*)(d_blob + parts[3].off);
+  int32_t* d_sce = (int32_t*)(d_blob + parts[4].off);
+  int32_t* d_nrep = (int32_t*)(d_blob + parts[5].off);
+  int32_t* d_repidx = (int32_t*)(d_blob + parts[6].off);
+  SegState* d_st = (SegState*)(d_blob + parts[7].off);
+  int64_t* d_lpx = (int64_t*)(d_blob + parts[8].off);
   const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
   int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
   int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len, live

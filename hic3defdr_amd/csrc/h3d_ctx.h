@@ -74,6 +74,9 @@ struct h3d_ctx {
   // pinned host word the disp loop polls (active work items), kept for the
   // ctx's lifetime (a per-call hipHostFree would synchronise the device)
   int32_t* h_meta = nullptr;
+  // pinned staging of estimate_disp's per-call tables (one H2D copy)
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
   // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
   // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
   // 1 (distance, total count)
