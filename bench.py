@@ -290,7 +290,11 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # H3D_DEVICE / H3D_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with
+    # several ranks on one GPU (RCCL needs one GPU per rank); the driver's
+    # runs use LOCAL_RANK's GPU and nccl
+    local = int(os.environ.get('H3D_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+    backend = os.environ.get('H3D_BENCH_BACKEND', 'nccl')
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_run(args.cpu_bins, args.dmax)   # before the GPU
@@ -299,7 +303,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl',
+                                    device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
 
     from hic3defdr_amd import _native, parallel
     ctx = _native.context(local)
