@@ -314,7 +314,11 @@ def main():
     tmp = tempfile.mkdtemp(prefix='h3dbench_r%d_' % rank)
     try:
         h, kw = make_workload(tmp, 'chrB%d' % rank, args.bins, args.dmax, rank)
-        h.prepare_data(verbose=False)
+        # this rank's own chromosome, prepared directly: the object's
+        # chrom=None path shards over the process group (LPT over ITS
+        # chromosome list -- here one per rank -- would leave rank > 0 idle)
+        for c in h.chroms:
+            h.prepare_data(chrom=c, verbose=False)
         raw, f, dist_np, _ = h._f_and_dist()
         design = kw['design']
         R, C = design.shape
