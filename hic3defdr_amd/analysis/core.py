@@ -1,6 +1,7 @@
 """Persistence mixin (reference hic3defdr/analysis/core.py): the outdir is the
 contract between stages — ``<outdir>/<name>_<chrom>.npy`` per chromosome,
 ``disp_per_dist.npy``, ``disp_fn_<cond>.pickle`` and ``pickle``."""
+import collections
 import os
 import pickle
 
@@ -122,18 +123,46 @@ class CoreHiC3DeFDR(object):
 
     # Write-through cache of the outdir arrays this object saved: a later
     # stage reading its own output back skips the disk read -- but only while
-    # the file on disk is still the one written (same inode, size and mtime),
-    # so edits or replacements of the outdir files are always seen.
+    # the file on disk is still the one written (same inode, size, mtime and
+    # ctime; a rewrite that restores the mtime still moves the ctime), so
+    # edits or replacements of the outdir files are always seen. Bounded: an
+    # LRU over the arrays' bytes, at most H3D_NPY_CACHE_BYTES (default
+    # 1 GiB; 0 turns the cache off), so a whole-genome run does not keep a
+    # second copy of every stage of every chromosome on the host.
+    _CACHE_BYTES = int(os.environ.get('H3D_NPY_CACHE_BYTES', 1 << 30))
+
     def _cache(self):
         c = self.__dict__.get('_npy_cache')
         if c is None:
-            c = self.__dict__['_npy_cache'] = {}
+            c = self.__dict__['_npy_cache'] = collections.OrderedDict()
+            self.__dict__['_npy_cache_bytes'] = 0
         return c
+
+    def _cache_drop(self, fname):
+        hit = self._cache().pop(fname, None)
+        if hit is not None:
+            self.__dict__['_npy_cache_bytes'] -= hit[1].nbytes
+
+    def _cache_put(self, fname, data):
+        self._cache_drop(fname)
+        cap = self._CACHE_BYTES
+        if data.nbytes > cap:
+            return
+        c = self._cache()
+        while c and self.__dict__['_npy_cache_bytes'] + data.nbytes > cap:
+            self._cache_drop(next(iter(c)))          # least recently used
+        c[fname] = (self._stamp(fname), data.copy())
+        self.__dict__['_npy_cache_bytes'] += data.nbytes
+
+    def cache_nbytes(self):
+        """Bytes held by the outdir cache."""
+        self._cache()
+        return self.__dict__['_npy_cache_bytes']
 
     @staticmethod
     def _stamp(fname):
         st = os.stat(fname)
-        return (st.st_ino, st.st_size, st.st_mtime_ns)
+        return (st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns)
 
     def _cached(self, fname):
         hit = self._cache().get(fname)
@@ -141,10 +170,11 @@ class CoreHiC3DeFDR(object):
             return None
         try:
             if self._stamp(fname) == hit[0]:
+                self._cache().move_to_end(fname)
                 return hit[1]
         except OSError:
             pass
-        del self._cache()[fname]
+        self._cache_drop(fname)
         return None
 
     def _read(self, fname, idx, col):
@@ -165,7 +195,9 @@ class CoreHiC3DeFDR(object):
         data = np.asanyarray(data)
         np.save(fname, data)
         if type(data) is np.ndarray:
-            self._cache()[fname] = (self._stamp(fname), data.copy())
+            self._cache_put(fname, data)
+        else:
+            self._cache_drop(fname)
 
     def load_data(self, name, chrom=None, idx=None, rep=None, cond=None,
                   coo=False):

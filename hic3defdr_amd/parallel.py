@@ -4,9 +4,9 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI;
 "gloo" works too). ``HiC3DeFDR.run_to_qvalues()`` under torchrun shards
 itself (``Shards``): every rank prepares and tests its own chromosomes and
 writes their outdir files (one shared outdir, as the reference's per-
-chromosome processes do); estimate_disp keeps the genome-wide pooling with
-the per-pass all-reduce below; BH gathers the loop pixels' p-values on rank 0
-and scatters the q-values back (``distributed_bh``).
+chromosome processes do); estimate_disp keeps the genome-wide pooling by a
+re-shard by distance; BH runs genome-wide on every rank over all-gathered
+p-values (``distributed_bh``).
 
 * prepare_data and lrt are independent per chromosome: chromosomes are
   assigned to ranks by greedy longest-processing-time on pixel counts
@@ -15,14 +15,19 @@ and scatters the q-values back (``distributed_bh``).
   analysis.py:169-206), so per-shard dispersions would NOT equal the
   reference. The segments (distance, condition) are independent of each
   other, so the pixels are re-sharded by DISTANCE for this stage
-  (``disp_per_dist_by_distance``): one all_to_all moves every disp pixel
-  (raw, f, dist: 12 R + 4 bytes) to the rank owning its distance (d mod
-  world), each rank runs the single-GPU driver -- every Brent search
-  in-kernel -- on the distances it owns, and one all-reduce of the D x C
-  table (owners' rows, zeros elsewhere) gives every rank the same
-  disp_per_dist. Two collectives per estimate_disp instead of one per data
-  pass; the only change from one GPU is the order of each segment's pixels
-  (ULP-level).
+  (``disp_per_dist_by_distance``): the distances go to ranks by LPT on
+  their genome-wide pixel counts (one all-reduce of a D-long count vector,
+  ``distance_owners``), one all_to_all moves every disp pixel (raw, f,
+  dist: 12 R + 4 bytes) to the rank owning its distance, each rank runs the
+  single-GPU driver -- every Brent search in-kernel -- on the distances it
+  owns, and one all-reduce of the D x C table (owners' rows, zeros
+  elsewhere) gives every rank the same disp_per_dist. The only change from
+  one GPU is the order of each segment's pixels (ULP-level).
+* BH (``distributed_bh`` / ``bh_all_ranks``): one all_gather of the
+  p-values (tensors on the rank's GPU under nccl); every rank runs the same
+  genome-wide BH on the gathered vector and keeps its own slice. BH's
+  q-values do not depend on the order of the p-values (tied p-values share
+  one q), so rank order instead of chromosome order changes no bit.
 * The per-pass alternative (``make_allreduce``, H3D_DISP_SHARD=pass) keeps
   the pixels in place and all-reduces the per-(distance, condition) NLL sums
   of every Brent step (D x C doubles, ~3 KB, ~54 passes per cfg2
@@ -56,12 +61,37 @@ class _CudaArray(object):
             'data': (int(ptr), False), 'version': 3, 'strides': None}
 
 
+def distance_owners(counts, world):
+    """Rank owning each distance: LPT over the distances by their genome-wide
+    pixel counts (`counts`, (D,)), so every rank gets about the same number
+    of pixels (the equalize and NLL work of a distance is proportional to its
+    pixels). Deterministic: every rank computes the same table."""
+    counts = np.asarray(counts, dtype=np.int64)
+    order = np.lexsort((np.arange(len(counts)), -counts))
+    loads = np.zeros(world, dtype=np.int64)
+    owner = np.zeros(len(counts), dtype=np.int32)
+    for d in order:
+        r = int(np.argmin(loads))        # first of the least loaded
+        owner[d] = r
+        loads[r] += counts[d]
+    return owner
+
+
+def _xdev(dev, group=None):
+    import torch
+    import torch.distributed as dist
+    # gloo exchanges host tensors
+    return dev if dist.get_backend(group) != 'gloo' else torch.device('cpu')
+
+
 def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
                               group=None):
     """estimate_disp's (D, C) disp_per_dist over every rank's pixels: the
-    pixels move to the rank owning their distance (d mod world) with ONE
-    all_to_all, each rank runs the single-GPU driver on what it received,
-    and ONE all-reduce of the owners' rows gives every rank the whole table.
+    distances go to ranks by LPT on their genome-wide pixel counts (one
+    all-reduce of D counts), the pixels move to the rank owning their
+    distance with ONE all_to_all, each rank runs the single-GPU driver on
+    what it received, and ONE all-reduce of the owners' rows gives every
+    rank the whole table.
 
     t_raw (n, R) int32, t_f (n, R) float64, t_dist (n,) int32: this rank's
     disp pixels on its GPU. libh3d must run on torch's current stream (a real
@@ -72,8 +102,16 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = t_raw.device
+    xdev = _xdev(dev, group)
     n, R = t_raw.shape
-    owner = t_dist.long() % world
+    dl = t_dist.long()
+    inb = (dl >= 0) & (dl < D)
+    cnt = torch.bincount(dl[inb], minlength=D)[:D].to(xdev)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+    owner_of = distance_owners(cnt.cpu().numpy(), world)
+    # distances outside [0, D) go to rank 0, whose driver rejects them
+    owner = torch.zeros(n, dtype=torch.int64, device=dev)
+    owner[inb] = torch.from_numpy(owner_of.astype(np.int64)).to(dev)[dl[inb]]
     order = torch.argsort(owner, stable=True)
     width = 12 * R + 4
 
@@ -86,8 +124,6 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
     rec = torch.cat([as_bytes(t_raw, 4 * R), as_bytes(t_f, 8 * R),
                      as_bytes(t_dist, 4)], dim=1)[order].contiguous()
     send = torch.bincount(owner, minlength=world)
-    # gloo exchanges host tensors
-    xdev = dev if dist.get_backend(group) != 'gloo' else torch.device('cpu')
     recv = torch.empty_like(send, device=xdev)
     dist.all_to_all_single(recv, send.to(xdev), group=group)
     s_list, r_list = send.tolist(), recv.tolist()
@@ -106,8 +142,7 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
         dist_m = torch.empty(0, dtype=torch.int32, device=dev)
     tab = ctx.disp_per_dist_dev(raw_m.data_ptr(), f_m.data_ptr(),
                                 dist_m.data_ptr(), m, R, cond_of_rep, C, D)
-    own = (np.arange(D) % world) == rank
-    tab[~own] = 0.0
+    tab[owner_of != rank] = 0.0
     t_tab = torch.from_numpy(tab).to(xdev)
     dist.all_reduce(t_tab, op=dist.ReduceOp.SUM, group=group)
     return t_tab.cpu().numpy()
@@ -159,6 +194,11 @@ class Shards(object):
                 self.world = dist.get_world_size()
                 self.rank = dist.get_rank()
                 self.dist = dist
+                if dist.get_backend() == 'nccl':
+                    # collectives (barrier, the BH all_gather) run on the
+                    # current device: this rank's GPU, not cuda:0
+                    import torch
+                    torch.cuda.set_device(device_for_rank())
         except ImportError:
             pass
         sizes = sizes or {c: 1 for c in chroms}
@@ -186,30 +226,53 @@ def chrom_sizes(bias_patterns, chroms):
     return out
 
 
+def gather_all(t, group=None):
+    """Every rank's 1-D tensor `t` (any length) concatenated in rank order,
+    on every rank (one all_gather of the lengths, one of the values padded
+    to the longest), and this rank's offset in it."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    xdev = _xdev(t.device, group)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=xdev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    top = max(ns + [1])
+    buf = torch.zeros(top, dtype=t.dtype, device=xdev)
+    buf[:t.numel()] = t.to(xdev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    allv = torch.cat([parts[r][:ns[r]] for r in range(world)])
+    return allv.to(t.device), int(sum(ns[:rank]))
+
+
+def bh_all_ranks(t_p, bh_fn, group=None):
+    """Genome-wide BH over every rank's p-values `t_p` (1-D float64 tensor):
+    each rank gathers all of them, runs `bh_fn` (tensor -> tensor, e.g. the
+    GPU BH) on the whole vector and returns its own slice of q."""
+    allp, off = gather_all(t_p, group)
+    return bh_fn(allp)[off:off + t_p.numel()]
+
+
 def distributed_bh(shards, pvalues, bh):
     """Genome-wide BH over every rank's p-values (analysis.py:286-303 over
     all chromosomes): ``pvalues`` maps this rank's chromosomes to arrays;
-    rank 0 gathers them (chromosome order of ``shards.assign``), applies
-    ``bh`` once and scatters each rank its chromosomes' q-values."""
+    ``bh`` maps a numpy vector to its q-values. Returns this rank's
+    chromosomes' q-values (dict)."""
+    import torch
     dist = shards.dist
-    gathered = [None] * shards.world if shards.rank == 0 else None
-    dist.gather_object(pvalues, gathered, dst=0)
-    scatter_in = None
-    if shards.rank == 0:
-        allp = {}
-        for part in gathered:
-            allp.update(part)
-        order = [c for r in range(shards.world) for c in shards.assign[r]]
-        order = sorted(order, key=lambda c: shards.order[c])
-        lens = [len(allp[c]) for c in order]
-        q = bh(np.concatenate([allp[c] for c in order])) if lens else []
-        off = np.concatenate([[0], np.cumsum(lens)]).astype(int)
-        qs = {c: q[off[i]:off[i + 1]] for i, c in enumerate(order)}
-        scatter_in = [{c: qs[c] for c in shards.assign[r]}
-                      for r in range(shards.world)]
-    out = [None]
-    dist.scatter_object_list(out, scatter_in, src=0)
-    return out[0]
+    mine = [c for c in shards.mine if c in pvalues]
+    local = np.concatenate([np.asarray(pvalues[c], dtype=np.float64)
+                            for c in mine]) if mine else np.zeros(0)
+    dev = torch.device('cuda', torch.cuda.current_device()) \
+        if dist.get_backend() == 'nccl' else torch.device('cpu')
+    q = bh_all_ranks(torch.from_numpy(local).to(dev),
+                     lambda t: torch.from_numpy(bh(t.cpu().numpy())))
+    q = q.cpu().numpy()
+    off = np.concatenate([[0], np.cumsum([len(pvalues[c]) for c in mine])])
+    return {c: q[off[i]:off[i + 1]] for i, c in enumerate(mine)}
 
 
 def device_for_rank():

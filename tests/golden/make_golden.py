@@ -592,6 +592,81 @@ def run_hard_cfg2(bins=20000, dmax=250, seed=0):
                         meta_seed=np.array(seed))
 
 
+def _ref_lrt_chunk(args):
+    from hic3defdr.util import lrt as lrt_mod
+    raw, f, dw, dsg = args
+    return lrt_mod.lrt(raw, f, dw, dsg)
+
+
+def run_full_cfg2(bins=20000, dmax=250, seed=0, chunk=20000, n_sample=50000):
+    """The headline workload (bench.py cfg2) through the REFERENCE at full
+    size: prepare_data + estimate_disp on the whole chromosome, then its
+    util/lrt.py:7-50 lrt over all disp pixels in chunks of `chunk` pixels
+    (SURVEY.md finding 5: chunking moves p by <= 2.1e-11 relative, and it
+    bounds the O(fail * N) brentq fallback of scaled_nb.py:162-181 by the
+    chunk), the p-values written back to the outdir and the reference's own
+    bh() (analysis.py:286-303) run on them. full_cfg2.npz: disp_per_dist,
+    a seeded sample of pixel indices with their p / q / llr / mu0 / mu1, the
+    2,000 smallest p-values with their q, and the sorted index lists of the
+    calls at q < 0.01 / 0.05 / 0.1."""
+    import multiprocessing
+    base = os.path.join('/tmp', 'h3golden_cfg2_data')
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, {'chrB0': bins}, dist_thresh_max=dmax,
+                                 seed=seed)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_cfg2_full_out')
+    shutil.rmtree(outdir, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax)
+    h.prepare_data(n_threads=-1, verbose=False)
+    h.estimate_disp(n_threads=-1)
+    chrom = kw['chroms'][0]
+    bias = h.load_bias(chrom)
+    sf = h.load_data('size_factors', chrom)
+    di = h.load_data('disp_idx', chrom)
+    row = h.load_data('row', chrom, idx=di)
+    col = h.load_data('col', chrom, idx=di)
+    raw = h.load_data('raw', chrom, idx=di)
+    disp = h.load_data('disp', chrom)
+    f = bias[row] * bias[col] * sf[di, :]
+    dsg = design.values
+    dw = np.dot(disp, dsg.T)
+    n = len(raw)
+    bounds = list(range(0, n, chunk)) + [n]
+    tasks = [(raw[a:b], f[a:b], dw[a:b], dsg)
+             for a, b in zip(bounds[:-1], bounds[1:])]
+    with multiprocessing.get_context('fork').Pool(8) as pool:
+        res = pool.map(_ref_lrt_chunk, tasks, chunksize=1)
+    p = np.concatenate([r[0] for r in res])
+    llr = np.concatenate([r[1] for r in res])
+    m0 = np.concatenate([r[2] for r in res])
+    m1 = np.concatenate([r[3] for r in res])
+    h.save_data(p, 'pvalues', chrom)
+    h.bh()
+    q = h.load_data('qvalues', chrom)
+    rng = np.random.default_rng(seed)
+    sample = np.sort(rng.choice(n, size=n_sample, replace=False))
+    out = {'disp_per_dist': np.load(os.path.join(outdir, 'disp_per_dist.npy')),
+           'sample_idx': sample.astype(np.int32), 'p': p[sample],
+           'q': q[sample], 'llr': llr[sample], 'mu0': m0[sample],
+           'mu1': m1[sample], 'n_disp_pixels': np.array(n),
+           'meta_bins': np.array(bins), 'meta_dmax': np.array(dmax),
+           'meta_seed': np.array(seed), 'meta_lrt_chunk': np.array(chunk),
+           'meta_equal_bin': np.array('stable')}
+    for fdr in (0.01, 0.05, 0.1):
+        out['calls_%g' % fdr] = np.where(q < fdr)[0].astype(np.int32)
+    # the smallest p-values (where the calls are decided): index, p, q
+    top = np.sort(np.argsort(p, kind='stable')[:2000])
+    out['top_idx'] = top.astype(np.int32)
+    out['top_p'] = p[top]
+    out['top_q'] = q[top]
+    np.savez_compressed(os.path.join(HERE, 'full_cfg2.npz'), **out)
+    print('full cfg2: %d disp px; calls' % n,
+          {k: len(v) for k, v in out.items() if k.startswith('calls_')})
+
+
 SIM_EVALS = [(None, None, False), (None, 15, False), (16, 30, True),
              (31, None, False)]
 
@@ -695,6 +770,8 @@ if __name__ == '__main__':
         run_lowess_drop()
     if 'hard_cfg2' in which:
         run_hard_cfg2()
+    if 'full_cfg2' in which:
+        run_full_cfg2()
     if 'sim' in which:
         run_sim()
     if 'alt' in which:

@@ -43,10 +43,43 @@ def test_file_changed_on_disk_wins():
     time.sleep(0.01)
     np.save(fname, np.ones(7))           # replaced behind the object's back
     np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'), np.ones(7))
+    h.save_data(np.zeros(5), 'disp_idx', 'chr1')   # cached again
     os.remove(fname)
     np.save(fname, np.full(5, 2.0))      # new inode, same size
     np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'),
                                   np.full(5, 2.0))
+
+
+def test_same_size_rewrite_in_place_with_mtime_restored():
+    h = _h()
+    h.save_data(np.zeros(5), 'disp_idx', 'chr1')
+    fname = os.path.join(h.outdir, 'disp_idx_chr1.npy')
+    st = os.stat(fname)
+    time.sleep(0.02)                     # past the clock tick of the ctime
+    with open(fname, 'r+b') as fh:       # same inode, same size
+        np.save(fh, np.full(5, 3.0))
+    os.utime(fname, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert os.stat(fname).st_mtime_ns == st.st_mtime_ns
+    assert os.stat(fname).st_ino == st.st_ino
+    np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'),
+                                  np.full(5, 3.0))
+
+
+def test_cache_is_bounded_lru(monkeypatch):
+    from hic3defdr_amd.analysis.core import CoreHiC3DeFDR
+    monkeypatch.setattr(CoreHiC3DeFDR, '_CACHE_BYTES', 3 * 800)
+    h = _h()
+    for i in range(10):                  # 10 chromosomes' worth of stages
+        h.save_data(np.full(100, float(i)), 'pvalues', 'chr%d' % i)
+        assert h.cache_nbytes() <= 3 * 800
+    assert h.cache_nbytes() == 3 * 800
+    for i in range(10):                  # evicted ones come from disk
+        np.testing.assert_array_equal(h.load_data('pvalues', 'chr%d' % i),
+                                      np.full(100, float(i)))
+    monkeypatch.setattr(CoreHiC3DeFDR, '_CACHE_BYTES', 0)
+    h2 = _h()
+    h2.save_data(np.zeros(10), 'pvalues', 'chr1')
+    assert h2.cache_nbytes() == 0
 
 
 def test_all_chroms_with_offsets_and_idx():

@@ -229,3 +229,79 @@ def test_distributed_bh_equals_single_process():
 def test_shards_single_process_owns_everything():
     sh = parallel.Shards(['a', 'b', 'c'])
     assert not sh.sharded and sh.mine == ['a', 'b', 'c'] and sh.rank == 0
+
+
+def test_distance_owners_lpt():
+    counts = np.array([0, 0, 50, 40, 30, 30, 20, 10])
+    own = parallel.distance_owners(counts, 3)
+    loads = np.bincount(own, weights=counts, minlength=3)
+    assert loads.max() - loads.min() <= counts.max()
+    assert sorted(set(own[2:])) == [0, 1, 2]
+    np.testing.assert_array_equal(own, parallel.distance_owners(counts, 3))
+    assert (parallel.distance_owners(counts, 1) == 0).all()
+
+
+GENOME = [150, 90, 130, 60, 110, 75, 140]     # a cfg3-shaped genome, small
+
+
+def _genome_worker(rank, world, port, result_file):
+    """cfg3's multi-GPU partition on gloo: chromosomes LPT-sharded, each rank
+    draws only its own (synthetic.draw_band seeds per chromosome), the
+    distance re-shard (LPT distance owners) for estimate_disp, and the
+    genome-wide BH over all ranks' p-values (bh_all_ranks)."""
+    import torch
+    import torch.distributed as dist
+    from hic3defdr_amd import synthetic
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    mine = parallel.lpt_assign({i: b for i, b in enumerate(GENOME)},
+                               world)[rank]
+    parts = synthetic.draw_genome(GENOME, (2, 2), D - 1, seed=4,
+                                  indices=sorted(mine))
+    raw = np.concatenate([p[0] for p in parts])
+    f = np.concatenate([p[1] for p in parts])
+    d = np.concatenate([p[2] for p in parts])
+    cond = np.array([0, 0, 1, 1], dtype=np.int32)
+    tab = parallel.disp_per_dist_by_distance(
+        _HostCtx(), torch.from_numpy(raw), torch.from_numpy(f),
+        torch.from_numpy(d), cond, 2, D)
+    # p-values stand-in: a deterministic function of each pixel's counts
+    p = torch.from_numpy((raw[:, 0] % 97 + 0.5) / 97.0 * 0.3)
+    q = parallel.bh_all_ranks(
+        p, lambda t: torch.from_numpy(oracle.adjust_pvalues(t.numpy())))
+    np.save(result_file % rank, {'tab': tab, 'mine': sorted(mine),
+                                 'q': q.numpy(), 'p': p.numpy()},
+            allow_pickle=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_genome_partition_world3_equals_single_process():
+    h3dbuild.build_hosttest()
+    from hic3defdr_amd import synthetic
+    world = 3
+    with tempfile.TemporaryDirectory() as tmp:
+        res = os.path.join(tmp, 'g%d.npy')
+        port = 29900 + (os.getpid() % 1000)
+        mp.spawn(_genome_worker, args=(world, port, res), nprocs=world,
+                 join=True)
+        outs = [np.load(res % r, allow_pickle=True).item()
+                for r in range(world)]
+    parts = synthetic.draw_genome(GENOME, (2, 2), D - 1, seed=4)
+    raw = np.concatenate([p[0] for p in parts])
+    f = np.concatenate([p[1] for p in parts])
+    d = np.concatenate([p[2] for p in parts])
+    single = _rounds(raw, f, d, np.array([0, 0, 1, 1]))
+    assert sorted(sum((o['mine'] for o in outs), [])) == list(range(len(GENOME)))
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o['tab'], outs[0]['tab'])
+    np.testing.assert_array_equal(np.isnan(outs[0]['tab']), np.isnan(single))
+    np.testing.assert_allclose(outs[0]['tab'], single, rtol=1e-6, atol=1e-12)
+    # genome-wide BH: every rank's slice = the single-process BH of its p
+    allp = np.concatenate([o['p'] for o in outs])
+    allq = oracle.adjust_pvalues(allp)
+    off = 0
+    for o in outs:
+        np.testing.assert_array_equal(o['q'], allq[off:off + len(o['p'])])
+        off += len(o['p'])

@@ -5,8 +5,10 @@ chromosome of 20k bins, R = 4, dist_thresh_max 250) on the GPU:
   O(fail * N) brentq fallback solves, scaled_nb.py:162-181) are held to the
   reference's own lrt on them (tests/golden/hard_cfg2.npz, made by
   tests/golden/make_golden.py run_hard_cfg2);
-- the whole chromosome through prepare_data -> estimate_disp -> lrt is held
-  to size-independent properties: no status flags, p in [0, 1], no NaN
+- the whole chromosome through the product's run_to_qvalues is held to the
+  reference's own run on it (tests/golden/full_cfg2.npz: disp_per_dist,
+  sampled p / q, the smallest p-values, identical call sets);
+- and to size-independent properties: no status flags, p in [0, 1], no NaN
   outside empty segments, and bit-identical results on a second call.
 """
 import os
@@ -48,6 +50,8 @@ def test_cfg2_secant_failure_pixels_vs_reference(ctx):
 
 @pytest.fixture(scope='module')
 def cfg2(ctx):
+    """The product's whole run_to_qvalues on the cfg2 chromosome (files in,
+    outdir out), its outdir arrays, and the disp pixels' raw / f / dist."""
     from hic3defdr_amd import HiC3DeFDR, synthetic
     tmp = tempfile.mkdtemp(prefix='h3d_cfg2_')
     try:
@@ -59,16 +63,48 @@ def cfg2(ctx):
                       bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
                       design=design, outdir=os.path.join(tmp, 'out'),
                       dist_thresh_max=250)
-        h.prepare_data(verbose=False)
+        h.run_to_qvalues(verbose=False)
+        chrom = kw['chroms'][0]
+        out = {st: h.load_data(st, chrom) for st in
+               ('pvalues', 'qvalues', 'llr', 'mu_hat_null', 'mu_hat_alt')}
+        out['disp_per_dist'] = h.load_data('disp_per_dist')
         raw, f, dist, _ = h._f_and_dist()
-        yield raw, f, dist, kw['design']
+        yield raw, f, dist, kw['design'], out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def test_cfg2_full_size_vs_reference(cfg2):
+    """The whole headline chromosome (3.76 M disp pixels) against the
+    reference's own prepare_data + estimate_disp + (chunked) lrt + bh on it
+    (tests/golden/full_cfg2.npz, make_golden.py run_full_cfg2): disp_per_dist,
+    p / q / llr / means on a seeded 50 k-pixel sample and on the 2,000
+    smallest p-values, and identical call sets at q < 0.01 / 0.05 / 0.1."""
+    g = golden('full_cfg2.npz')
+    _, _, _, _, out = cfg2
+    assert len(out['pvalues']) == int(g['n_disp_pixels'])
+    dpd, ref = out['disp_per_dist'], g['disp_per_dist']
+    np.testing.assert_array_equal(np.isnan(dpd), np.isnan(ref))
+    assert rel_err(dpd, ref) < RTOL_PQ
+    s = g['sample_idx']
+    assert rel_err(out['pvalues'][s], g['p']) < RTOL_PQ
+    assert rel_err(out['qvalues'][s], g['q']) < RTOL_PQ
+    assert rel_err(out['mu_hat_null'][s], g['mu0']) < RTOL_PQ
+    assert rel_err(out['mu_hat_alt'][s], g['mu1']) < RTOL_PQ
+    # llr crosses zero: absolute, scaled to its magnitude
+    assert np.max(np.abs(out['llr'][s] - g['llr']) /
+                  np.maximum(np.abs(g['llr']), 1.0)) < RTOL_PQ
+    t = g['top_idx']
+    assert rel_err(out['pvalues'][t], g['top_p']) < RTOL_PQ
+    assert rel_err(out['qvalues'][t], g['top_q']) < RTOL_PQ
+    for fdr in (0.01, 0.05, 0.1):
+        np.testing.assert_array_equal(
+            np.where(out['qvalues'] < fdr)[0], g['calls_%g' % fdr])
+
+
 def test_cfg2_full_size_properties(ctx, cfg2):
     from hic3defdr_amd import _native
-    raw, f, dist, design = cfg2
+    raw, f, dist, design, _ = cfg2
     assert len(raw) == int(golden('hard_cfg2.npz')['n_disp_pixels'])
     cond = design.argmax(axis=1)
     C, D = design.shape[1], 251

@@ -8,11 +8,9 @@ inputs.
     cfg4: human chr1 at 5 kb -- 49,792 bins, R = 18 (6 + 6 + 6), C = 3,
           dist_thresh_max 400 (chi2 df = 2, k_lrt<32, 8>, the M = 8 disp path)
 
-The pixels are drawn directly in the band (no files; the SURVEY §8(d)
-generator's model: mu(d) = 400 (d+1)^-1, 0.2 % loops x5, 1 % differential
-x2 in conditions >= 1, per-bin bias exp(N(0, .25)), depth 0.8 + 0.1 k,
-NB(1/0.05)); disp_idx = every condition's mean of raw / (b_i b_j) >= 1 and
-d >= 4, as prepare_data with unit size factors. Prints one JSON line.
+The pixels are drawn directly in the band (synthetic.draw_band: no files,
+the SURVEY §8(d) generator's model with unit size factors). Prints one JSON
+line.
 
     python tools/run_cfg.py --cfg 3 [--steps 3 --warmup 1]
 """
@@ -27,47 +25,26 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-MM10 = [19535, 18211, 16007, 15649, 15171, 14950, 14546, 12930, 12459, 13069,
-        12208, 12013, 12042, 12490, 10404, 9820, 9499, 9070, 6143, 17102]
+from hic3defdr_amd.synthetic import MM10_BINS  # noqa: E402
+
 CFGS = {
-    3: dict(chroms=MM10, npc=(2, 2), dmax=200),
+    3: dict(chroms=MM10_BINS, npc=(2, 2), dmax=200),
     4: dict(chroms=[49792], npc=(6, 6, 6), dmax=400),
 }
 
 
 def draw(bins_list, npc, dmax, seed=0):
-    rng = np.random.default_rng(seed)
-    R = sum(npc)
+    from hic3defdr_amd import synthetic
+    parts = []
+    for i, n_bins in enumerate(bins_list):
+        parts.append(synthetic.draw_band(n_bins, npc, dmax, seed=seed,
+                                         chrom_index=i))
+        print('  chrom of %d bins: %d disp px' % (n_bins, len(parts[-1][0])),
+              file=sys.stderr, flush=True)
     cond = np.repeat(np.arange(len(npc)), npc).astype(np.int32)
-    raws, fs, dists = [], [], []
-    for n_bins in bins_list:
-        d = np.concatenate([np.full(n_bins - k, k, dtype=np.int32)
-                            for k in range(min(dmax, n_bins - 1) + 1)])
-        r = np.concatenate([np.arange(n_bins - k, dtype=np.int32)
-                            for k in range(min(dmax, n_bins - 1) + 1)])
-        c = r + d
-        base = 400.0 / (d + 1.0)
-        base *= np.where(rng.random(d.size) < 0.002, 5.0, 1.0)
-        diff = rng.random(d.size) < 0.01
-        raw = np.empty((d.size, R), dtype=np.int32)
-        f = np.empty((d.size, R))
-        for k in range(R):
-            b = np.exp(rng.normal(0, 0.25, n_bins))
-            bb = b[r] * b[c]
-            mu = base * np.where(diff & (cond[k] >= 1), 2.0, 1.0) * bb * \
-                (0.8 + 0.1 * (k % 4))
-            raw[:, k] = rng.negative_binomial(20.0, 20.0 / (20.0 + mu))
-            f[:, k] = bb
-        keep = d >= 4
-        for ci in range(len(npc)):
-            keep &= (raw[:, cond == ci] / f[:, cond == ci]).mean(axis=1) >= 1.0
-        raws.append(raw[keep])
-        fs.append(f[keep])
-        dists.append(d[keep])
-        print('  chrom of %d bins: %d band px, %d disp px' %
-              (n_bins, d.size, keep.sum()), file=sys.stderr, flush=True)
-    return (np.concatenate(raws), np.concatenate(fs), np.concatenate(dists),
-            cond)
+    return (np.concatenate([p[0] for p in parts]),
+            np.concatenate([p[1] for p in parts]),
+            np.concatenate([p[2] for p in parts]), cond)
 
 
 def main():
