@@ -1,24 +1,33 @@
 """Benchmark: pixels/sec through estimate_disp + lrt (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "cfg2"): per GPU one synthetic
-chromosome of 20,000 bins, 4 replicates (2 + 2 conditions), dist_thresh_max
-250 (SURVEY.md §8(d) generator, seed = rank). Untimed setup: generate the
-input files, run the product's GPU prepare_data, upload raw / f / dist of the
-disp pixels to HBM. One step = estimate_disp (qcml per distance x condition,
-lowess smoothing table) + lrt (fused per-pixel GLM fits + LRT) on the
-resident inputs, outputs left in HBM.
+Workloads (BASELINE.json configs):
+- cfg2 (configs[1], the N = 1 default): one synthetic chromosome of 20,000
+  bins, 4 replicates (2 + 2 conditions), dist_thresh_max 250 (SURVEY.md §8(d)
+  generator, seed = rank). Untimed setup: generate the input files, run the
+  product's GPU prepare_data, upload raw / f / dist of the disp pixels to
+  HBM. One step = estimate_disp (qcml per distance x condition, lowess
+  smoothing table) + lrt (fused per-pixel GLM fits + LRT) on the resident
+  inputs, outputs left in HBM.
+- cfg3 (configs[2], the N > 1 default; --config cfg3 at any N): the whole
+  mouse genome at 10 kb -- 20 mm10-sized chromosomes, 4 replicates, dmax 200,
+  ~46 M disp pixels -- STRONG scaling: the chromosomes are LPT-sharded over
+  the ranks, each rank draws only its own (synthetic.draw_band, no files)
+  and holds them in HBM. One step = estimate_disp over the whole genome (the
+  distance re-shard: distances LPT-assigned by pixel count, one all_to_all
+  of the disp pixels, the single-GPU driver per rank, one all-reduce of the
+  D x C table) + lowess tables + lrt of the rank's own pixels + the
+  genome-wide BH (one all_gather of the p-values, the GPU BH on every rank).
 
-N > 1 (torchrun, one rank per GPU over RCCL): weak scaling -- every rank owns
-its own chromosome; the genome-wide per-distance pooling of estimate_disp is
-kept by an all-reduce of the per-segment NLL sums each data pass.
-
-The CPU baseline (rank 0, N = 1) runs FIRST, before anything touches the GPU
-(its worker pool forks): the CPU restatement (oracle/, numpy/scipy) with the
-reference's parallel structure on min(os.cpu_count(), 16) processes, median
-of 4 runs, on a bounded sample; two rows: fallback-fixed (brentq only on the
-failed pixel) and faithful (the reference's O(fail * N) brentq fallback,
+The CPU baseline (rank 0, N = 1, cfg2) runs FIRST, before anything touches
+the GPU (its worker pool forks): the CPU restatement (oracle/, numpy/scipy)
+with the reference's parallel structure on min(os.cpu_count(), 16)
+processes (16 = the GPU box's CPU share per GPU): the fallback-fixed row
+(brentq only on the failed pixel) on the FULL cfg2 chromosome, and the
+faithful row (the reference's O(fail * N) brentq fallback,
 scaled_nb.py:162-181, LRT on one process per chromosome as
-analysis.py:247-257).
+analysis.py:247-257) on a 1,000-bin sample -- its O(fail * N) cost grows
+super-linearly with the chromosome, so the survey's own measurement of the
+reference at cfg2 is quoted beside it.
 
 Prints ONE JSON line on rank 0.
 """
@@ -147,8 +156,16 @@ def cpu_pipeline(pool, workers, raw, f, dist, design, D, faithful):
         _lrt_task, [(raw[b], f[b], dw[b], design, False) for b in blocks]))
 
 
-def cpu_baseline_run(bins, dmax, seed=123):
-    import multiprocessing
+# SURVEY.md §6 [probe]: the reference itself on cfg2 (20k bins, dmax 250;
+# 3,774,156 disp pixels), n_threads=-1 on 8 cores: estimate_disp 35.69 s +
+# lrt 3,167.8 s (3,281 brentq fallbacks, O(fail * N) each)
+SURVEY_REF_CFG2 = {'value': 1178.0, 'unit': 'pixels/s', 'cores': 8,
+                   'kind': 'reference',
+                   'source': 'SURVEY.md section 6: the reference on cfg2 in '
+                             'the survey container (Xeon, 8 cores)'}
+
+
+def _cpu_inputs(bins, dmax, seed):
     import oracle
     from hic3defdr_amd import synthetic
     tmp = tempfile.mkdtemp(prefix='h3dbench_cpu_')
@@ -164,44 +181,75 @@ def cpu_baseline_run(bins, dmax, seed=123):
         shutil.rmtree(tmp, ignore_errors=True)
     di = prep['disp_idx']
     row, col = prep['row'][di], prep['col'][di]
-    raw = prep['raw'][di]
-    f = bias[row] * bias[col] * prep['size_factors'][di]
-    dist = col - row
-    n = len(raw)
+    return {'raw': prep['raw'][di],
+            'f': bias[row] * bias[col] * prep['size_factors'][di],
+            'dist': col - row, 'design': design}
+
+
+def _cpu_rows(pool, workers, inp, dmax, faithful, runs):
+    import oracle
+    times, p = [], None
+    for _ in range(runs):
+        oracle.STATS['brentq_fallbacks'] = 0
+        t0 = time.perf_counter()
+        p = cpu_pipeline(pool, workers, inp['raw'], inp['f'], inp['dist'],
+                         inp['design'], dmax + 1, faithful)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {'value': len(inp['raw']) / med, 'median_s': med,
+            'runs_s': times}, p
+
+
+def cpu_baseline_run(full_bins, sample_bins, dmax, seed=123, full_runs=1):
+    """fallback-fixed row on the full chromosome (`full_bins`; the headline
+    workload's shape), faithful row on the `sample_bins` sample."""
+    import multiprocessing
+    import oracle
     ncpu = os.cpu_count() or 1
     workers = max(1, min(ncpu, 16))   # the GPU box's CPU share per GPU
-    rows, p_out = {}, {}
+    full = _cpu_inputs(full_bins, dmax, seed) if full_bins else None
+    sample = _cpu_inputs(sample_bins, dmax, seed)
     ctx = multiprocessing.get_context('fork')
     with ctx.Pool(workers) as pool:
-        for faithful in (False, True):
-            times = []
-            for _ in range(CPU_RUNS):
-                t0 = time.perf_counter()
-                p = cpu_pipeline(pool, workers, raw, f, dist, design, dmax + 1,
-                                 faithful)
-                times.append(time.perf_counter() - t0)
-            med = statistics.median(times)
-            rows[faithful] = {'value': n / med, 'median_s': med,
-                              'runs_s': times}
-            p_out[faithful] = p
-    sample = ('1 synthetic chrom of %d bins (seed %d), dmax %d, 4 reps 2+2: '
-              '%d disp pixels; median of %d runs' % (bins, seed, dmax, n,
-                                                     CPU_RUNS))
-    base = {'value': rows[False]['value'], 'unit': 'pixels/s',
-            'cores': workers, 'cpu_count': ncpu, 'kind': 'port',
+        if full is not None:
+            fixed, _ = _cpu_rows(pool, workers, full, dmax, False, full_runs)
+        s_fixed, p_fixed = _cpu_rows(pool, workers, sample, dmax, False,
+                                     CPU_RUNS)
+        s_faith, p_faith = _cpu_rows(pool, workers, sample, dmax, True,
+                                     CPU_RUNS)
+    # the faithful row's cost is its secant failures x the chromosome's
+    # pixels: the brentq fallbacks of its (in-process) LRT, last run
+    n_fail = int(oracle.STATS['brentq_fallbacks'])
+    if full is None:
+        fixed = s_fixed
+    n_full = len(full['raw']) if full is not None else len(sample['raw'])
+    base = {'value': fixed['value'], 'unit': 'pixels/s', 'cores': workers,
+            'cpu_count': ncpu, 'kind': 'port',
             'variant': 'fallback-fixed (brentq on the failed pixel only; '
                        'LRT over pixel blocks on the pool)',
-            'median_s': rows[False]['median_s'],
-            'runs_s': rows[False]['runs_s'], 'sample': sample,
-            'faithful': {'value': rows[True]['value'], 'unit': 'pixels/s',
-                         'cores': workers,
-                         'variant': 'faithful O(fail*N) brentq '
-                                    '(scaled_nb.py:162-181); qcml on the '
-                                    'pool, LRT one process per chromosome',
-                         'median_s': rows[True]['median_s'],
-                         'runs_s': rows[True]['runs_s']}}
-    return base, {'raw': raw, 'f': f, 'dist': dist, 'design': design,
-                  'p_fixed': p_out[False], 'p_faithful': p_out[True]}
+            'median_s': fixed['median_s'], 'runs_s': fixed['runs_s'],
+            'sample': '1 synthetic chrom of %d bins (seed %d), dmax %d, 4 '
+                      'reps 2+2: %d disp pixels -- the headline workload '
+                      'shape; %d run(s)' % (full_bins or sample_bins, seed,
+                                            dmax, n_full, full_runs),
+            'fallback_fixed_on_sample': dict(s_fixed, pixels=len(
+                sample['raw'])),
+            'faithful': {
+                'value': s_faith['value'], 'unit': 'pixels/s',
+                'cores': workers,
+                'variant': 'faithful O(fail*N) brentq (scaled_nb.py:162-181);'
+                           ' qcml on the pool, LRT one process per chromosome',
+                'sample': '%d-bin chromosome (seed %d): %d disp pixels, %d '
+                          'LRT brentq fallbacks; median of %d runs'
+                          % (sample_bins, seed, len(sample['raw']), n_fail,
+                             CPU_RUNS),
+                'median_s': s_faith['median_s'], 'runs_s': s_faith['runs_s'],
+                'note': 'per-pixel cost grows with failures x chromosome '
+                        'pixels; at cfg2 size see reference_at_cfg2'},
+            'reference_at_cfg2': SURVEY_REF_CFG2}
+    return base, {'raw': sample['raw'], 'f': sample['f'],
+                  'dist': sample['dist'], 'design': sample['design'],
+                  'p_fixed': p_fixed, 'p_faithful': p_faith}
 
 
 def sample_parity(ctx, sample, dmax):
@@ -271,46 +319,151 @@ def e2e_wall(h, tmp):
                     'NPZ parse and .npy outdir writes included'}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=3)
-    ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--bins', type=int, default=20000)
-    ap.add_argument('--dmax', type=int, default=250)
-    ap.add_argument('--cpu-bins', type=int, default=1000)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-e2e', action='store_true')
-    ap.add_argument('--noop-reduce', action='store_true',
-                    help='measurement: run the multi-rank estimate_disp driver '
-                         '(per-pass NLL sums through the reduce hook) on one '
-                         'GPU with a no-op reduce, i.e. the N > 1 kernel and '
-                         'host-sync path without the collective')
-    args = ap.parse_args()
+def _outputs(torch, dev, n, C):
+    t_p = torch.empty(n, dtype=torch.float64, device=dev)
+    return {'p': t_p, 'llr': torch.empty_like(t_p), 'mu0': torch.empty_like(t_p),
+            'q': torch.empty_like(t_p),
+            'mu1': torch.empty((n, C), dtype=torch.float64, device=dev),
+            'disp': torch.empty((n, C), dtype=torch.float64, device=dev)}
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    # H3D_DEVICE / H3D_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with
-    # several ranks on one GPU (RCCL needs one GPU per rank); the driver's
-    # runs use LOCAL_RANK's GPU and nccl
-    local = int(os.environ.get('H3D_DEVICE', os.environ.get('LOCAL_RANK', '0')))
-    backend = os.environ.get('H3D_BENCH_BACKEND', 'nccl')
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_run(args.cpu_bins, args.dmax)   # before the GPU
+
+def _upload(torch, dev, raw, f, dist_np):
+    return (torch.from_numpy(np.ascontiguousarray(raw, dtype=np.int32)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(f)).to(dev),
+            torch.from_numpy(np.ascontiguousarray(dist_np, dtype=np.int32)).to(dev))
+
+
+def timed_run(args, ctx, dist, dev, step):
+    """W untimed steps, then exactly K timed steps between barrier +
+    synchronize on both sides (HIP events on the roofline kernels inside),
+    then one untimed step with every kernel scope timed. Returns
+    (elapsed max over ranks, roofline-kernel events, per-kernel ms)."""
     import torch
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == 'nccl':
-            dist.init_process_group('nccl',
-                                    device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(backend)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.profile_reset()
+    ctx.profile(True, level=1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.profile(False)
+    ev = {k: ctx.profile_read(k) for k in ('disp_work', 'lrt')}
+    ctx.profile_reset()
+    ctx.profile(True, level=2)
+    step()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    per = {k: ctx.profile_read(k) for k in
+           ('disp_reduce', 'disp_update', 'disp_nll', 'disp_prep', 'disp_work',
+            'lrt')}
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, ev, per
 
+
+def total_over_ranks(dist, dev, n):
+    if not dist:
+        return n
+    import torch
+    t = torch.tensor([n], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
+               dmax, workload, parallelism, scaling):
+    w_ms, w_n, w_bytes = ev['disp_work']
+    l_ms, l_n, _ = ev['lrt']
+    n_ms, n_n, n_bytes = per['disp_nll']
+    w_avg_s = (w_ms / max(w_n, 1)) / 1e3
+    w_bpl = w_bytes / max(w_n, 1)
+    w_ach = w_bpl / w_avg_s / 1e9 if w_avg_s else 0.0
+    l_avg_s = (l_ms / max(l_n, 1)) / 1e3
+    l_ach = (n_local * bytes_per_lrt_pixel(R, C)) / l_avg_s / 1e9 \
+        if l_avg_s else 0.0
+    n_avg_s = (n_ms / max(n_n, 1)) / 1e3
+    # R_c = 2 runs the M = 2 instantiation (libh3d default; M = 4 with
+    # H3D_DISP_M2=0): whichever the committed summary measured
+    eq_pmc = pmc_kernel('k_disp_work<2, 4, 0, false>', bins, dmax) \
+        or pmc_kernel('k_disp_work<4, 4, 0, false>', bins, dmax)
+    nll_pmc = pmc_kernel('k_brent_gang<2>', bins, dmax) \
+        or pmc_kernel('k_brent<2>', bins, dmax) \
+        or pmc_kernel('k_brent<4>', bins, dmax)
+    lrt_pmc = pmc_kernel('k_lrt<4, 2>', bins, dmax)
+    eq_fp64 = fp64_roof(eq_pmc, w_avg_s)
+    roof = {
+        'bound': 'fp64', 'kernel': 'k_disp_work<2,4,kEqualize,false> (equalize pass)',
+        'achieved': eq_fp64['achieved'] if eq_fp64 else None,
+        'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+        'frac': eq_fp64['frac'] if eq_fp64 else None,
+        'useful_frac': eq_fp64.get('useful_frac') if eq_fp64 else None,
+        'lane_util': eq_pmc['lane_util'] if eq_pmc else None,
+        'flops_per_launch': eq_pmc['f64_flops'] if eq_pmc else None,
+        'flops_source': 'FP64 flops issued per launch, PMC '
+                        '(ADD+MUL+TRANS+2*FMA)_F64 x 64 lanes, '
+                        'profiles/pmc_default.json; useful_frac = '
+                        'frac x lane_util',
+        'traffic': eq_pmc['hbm_bytes'] if eq_pmc else None,
+        'traffic_source': 'PMC HBM bytes per launch (FETCH_SIZE x2 '
+                          '+ WRITE_SIZE), profiles/pmc_default.json',
+        'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
+        'hbm': {'achieved': w_ach, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'frac': w_ach / HBM_PEAK_GBS,
+                'bytes_per_launch': w_bpl,
+                'note': 'algorithmic: 20 B per equalize pixel-'
+                        'replicate (raw 4 + f 8 in, pseudodata 8 '
+                        'out)'},
+        'note': 'FP64-VALU bound (SURVEY.md finding 3): q2qnbinom '
+                'incomplete-gamma series / continued fractions'}
+    kernels = {k: v[0] for k, v in per.items()}
+    kernels['note'] = 'one extra untimed step, every kernel timed (rank 0)'
+    return {
+        'metric': METRIC, 'value': tot_px * args.steps / elapsed,
+        'unit': 'pixels/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True, 'scaling': scaling,
+        'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (SURVEY.md 8(d) generator; no demo data '
+                'offline)',
+        'config': {'workload': workload, 'disp_pixels_rank0': n_local,
+                   'disp_pixels_total': tot_px, 'parallelism': parallelism},
+        'roofline': roof,
+        'kernel_rooflines': {
+            'nll_brent': {
+                'fp64': fp64_roof(nll_pmc, n_avg_s),
+                'hbm_traffic_per_launch': nll_pmc['hbm_bytes']
+                if nll_pmc else None,
+                'algorithmic_bytes_per_launch': n_bytes / max(n_n, 1),
+                'avg_launch_us': n_avg_s * 1e6},
+            'lrt': {'fp64': fp64_roof(lrt_pmc, l_avg_s),
+                    'hbm': {'achieved': l_ach, 'peak': HBM_PEAK_GBS,
+                            'unit': 'GB/s', 'frac': l_ach / HBM_PEAK_GBS,
+                            'bytes_per_pixel': bytes_per_lrt_pixel(R, C)},
+                    'hbm_traffic_per_launch': lrt_pmc['hbm_bytes']
+                    if lrt_pmc else None,
+                    'avg_launch_us': l_avg_s * 1e6}},
+        'kernels_ms_per_step': kernels,
+        'work_per_step': {
+            'equalize_pixel_reps': w_bytes / 20.0 / args.steps,
+            'nll_pixel_reps': n_bytes / 8.0,
+            'equalize_launches': w_n / args.steps},
+    }
+
+
+def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
+    """Weak scaling: one 20k-bin chromosome per rank (BASELINE configs[1])."""
+    import torch
     from hic3defdr_amd import _native, parallel
-    ctx = _native.context(local)
     tmp = tempfile.mkdtemp(prefix='h3dbench_r%d_' % rank)
     try:
         h, kw = make_workload(tmp, 'chrB%d' % rank, args.bins, args.dmax, rank)
@@ -325,17 +478,10 @@ def main():
         D = args.dmax + 1
         cond = design.argmax(axis=1).astype(np.int32)
         n = len(raw)
-        dev = torch.device('cuda', local)
-        t_raw = torch.from_numpy(raw.astype(np.int32)).to(dev).contiguous()
-        t_f = torch.from_numpy(f).to(dev).contiguous()
-        t_dist = torch.from_numpy(dist_np.astype(np.int32)).to(dev)
-        t_p = torch.empty(n, dtype=torch.float64, device=dev)
-        t_llr = torch.empty_like(t_p)
-        t_mu0 = torch.empty_like(t_p)
-        t_mu1 = torch.empty((n, C), dtype=torch.float64, device=dev)
-        t_disp = torch.empty_like(t_mu1)
+        t_raw, t_f, t_dist = _upload(torch, dev, raw, f, dist_np)
+        o = _outputs(torch, dev, n, C)
         torch.cuda.synchronize()
-        # libh3d and the RCCL all-reduce share one real stream (torch's
+        # libh3d and the RCCL collectives share one real stream (torch's
         # default stream has handle 0 = "the ctx's own stream" to libh3d)
         stream = torch.cuda.Stream(dev)
         torch.cuda.set_stream(stream)
@@ -360,146 +506,170 @@ def main():
                                             D, reduce=reduce)
             tab = _native.disp_tables(dpd)
             ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
-                        tab, n, R, cond, t_p.data_ptr(), t_llr.data_ptr(),
-                        t_mu0.data_ptr(), t_mu1.data_ptr(), t_disp.data_ptr())
+                        tab, n, R, cond, o['p'].data_ptr(), o['llr'].data_ptr(),
+                        o['mu0'].data_ptr(), o['mu1'].data_ptr(),
+                        o['disp'].data_ptr())
             return dpd
 
-        for _ in range(args.warmup):
-            step()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        # timed region: HIP events around the roofline kernels only
-        ctx.profile_reset()
-        ctx.profile(True, level=1)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        ctx.profile(False)
-        w_ms, w_n, w_bytes = ctx.profile_read('disp_work')
-        l_ms, l_n, l_px = ctx.profile_read('lrt')
-        # one more (untimed) step with every kernel scope timed, for the
-        # per-kernel breakdown
-        ctx.profile_reset()
-        ctx.profile(True, level=2)
-        step()
-        torch.cuda.synchronize()
-        ctx.profile(False)
-        r_ms, r_n, _ = ctx.profile_read('disp_reduce')
-        u_ms, u_n, _ = ctx.profile_read('disp_update')
-        n_ms, n_n, n_bytes = ctx.profile_read('disp_nll')
-        p_ms, p_n, _ = ctx.profile_read('disp_prep')
-        b_ms, b_n, _ = ctx.profile_read('disp_work')
-        b_lrt, _, _ = ctx.profile_read('lrt')
-        tot_px = n
-        if dist:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-            t = torch.tensor([n], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            tot_px = int(t.item())
-        value = tot_px * args.steps / elapsed
-        if rank == 0:
-            w_avg_s = (w_ms / max(w_n, 1)) / 1e3
-            w_bpl = w_bytes / max(w_n, 1)
-            w_ach = w_bpl / w_avg_s / 1e9 if w_avg_s else 0.0
-            l_avg_s = (l_ms / max(l_n, 1)) / 1e3
-            l_ach = (n * bytes_per_lrt_pixel(R, C)) / l_avg_s / 1e9 \
-                if l_avg_s else 0.0
-            n_avg_s = (n_ms / max(n_n, 1)) / 1e3
-            # R_c = 2 runs the M = 2 instantiation (libh3d default; M = 4
-            # with H3D_DISP_M2=0): whichever the committed summary measured
-            eq_pmc = pmc_kernel('k_disp_work<2, 4, 0, false>', args.bins, args.dmax) \
-                or pmc_kernel('k_disp_work<4, 4, 0, false>', args.bins, args.dmax)
-            nll_pmc = pmc_kernel('k_brent<2>', args.bins, args.dmax) \
-                or pmc_kernel('k_brent<4>', args.bins, args.dmax)
-            lrt_pmc = pmc_kernel('k_lrt<4, 2>', args.bins, args.dmax)
-            eq_fp64 = fp64_roof(eq_pmc, w_avg_s)
-            roof = {
-                'bound': 'fp64', 'kernel': 'k_disp_work<2,4,kEqualize,false> (equalize pass)',
-                'achieved': eq_fp64['achieved'] if eq_fp64 else None,
-                'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': eq_fp64['frac'] if eq_fp64 else None,
-                'useful_frac': eq_fp64.get('useful_frac') if eq_fp64 else None,
-                'lane_util': eq_pmc['lane_util'] if eq_pmc else None,
-                'flops_per_launch': eq_pmc['f64_flops'] if eq_pmc else None,
-                'flops_source': 'FP64 flops issued per launch, PMC '
-                                '(ADD+MUL+TRANS+2*FMA)_F64 x 64 lanes, '
-                                'profiles/pmc_default.json; useful_frac = '
-                                'frac x lane_util',
-                'traffic': eq_pmc['hbm_bytes'] if eq_pmc else None,
-                'traffic_source': 'PMC HBM bytes per launch (FETCH_SIZE x2 '
-                                  '+ WRITE_SIZE), profiles/pmc_default.json',
-                'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
-                'hbm': {'achieved': w_ach, 'peak': HBM_PEAK_GBS,
-                        'unit': 'GB/s', 'frac': w_ach / HBM_PEAK_GBS,
-                        'bytes_per_launch': w_bpl,
-                        'note': 'algorithmic: 20 B per equalize pixel-'
-                                'replicate (raw 4 + f 8 in, pseudodata 8 '
-                                'out)'},
-                'note': 'FP64-VALU bound (SURVEY.md finding 3): q2qnbinom '
-                        'incomplete-gamma series / continued fractions'}
-            out = {
-                'metric': METRIC, 'value': value, 'unit': 'pixels/s',
-                'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-                'ms_per_step': elapsed / args.steps * 1e3,
-                'higher_is_better': True, 'scaling': 'weak',
-                'vs_baseline': None, 'dtype': 'f64',
-                'data': 'synthetic (SURVEY.md 8(d) generator; no demo data '
-                        'offline)',
-                'config': {
-                    'workload': 'cfg2: per GPU 1 chrom x %d bins, 4 reps '
-                                '(2+2), dist_thresh_max %d, estimate_disp '
-                                '(qcml) + lrt on HBM-resident inputs'
-                                % (args.bins, args.dmax),
-                    'disp_pixels_per_gpu': n, 'disp_pixels_total': tot_px,
-                    'parallelism': 'dp%d (chromosome shards; %s)' % (
-                        world, 'per-pass NLL sums, no-op reduce (the N > 1 '
-                        'driver on one GPU)' if reduce and world == 1 else
-                        'in-kernel Brent searches' if world == 1 else
-                        'distance re-shard: all_to_all of the disp pixels, '
-                        'in-kernel Brent per rank, table all-reduce' if by_dist
-                        else 'per-pass NLL all-reduce over RCCL')},
-                'roofline': roof,
-                'kernel_rooflines': {
-                    'nll_k_brent': {
-                        'fp64': fp64_roof(nll_pmc, n_avg_s),
-                        'hbm_traffic_per_launch': nll_pmc['hbm_bytes']
-                        if nll_pmc else None,
-                        'algorithmic_bytes_per_launch': n_bytes / max(n_n, 1),
-                        'avg_launch_us': n_avg_s * 1e6},
-                    'lrt': {'fp64': fp64_roof(lrt_pmc, l_avg_s),
-                            'hbm': {'achieved': l_ach, 'peak': HBM_PEAK_GBS,
-                                    'unit': 'GB/s',
-                                    'frac': l_ach / HBM_PEAK_GBS,
-                                    'bytes_per_pixel':
-                                        bytes_per_lrt_pixel(R, C)},
-                            'hbm_traffic_per_launch': lrt_pmc['hbm_bytes']
-                            if lrt_pmc else None,
-                            'avg_launch_us': l_avg_s * 1e6}},
-                'kernels_ms_per_step': {
-                    'note': 'one extra untimed step, every kernel timed',
-                    'disp_work': b_ms, 'disp_reduce': r_ms,
-                    'disp_update': u_ms, 'disp_nll': n_ms,
-                    'disp_prep': p_ms, 'lrt': b_lrt},
-                'work_per_step': {
-                    'equalize_pixel_reps': w_bytes / 20.0 / args.steps,
-                    'nll_pixel_reps': n_bytes / 8.0,
-                    'disp_launches': b_n, 'equalize_launches': w_n / args.steps},
-            }
-            if cpu is not None:
-                out['cpu_baseline'] = cpu[0]
-                out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
-            if world == 1 and not args.no_e2e:
-                out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
-            print(json.dumps(out), flush=True)
+        elapsed, ev, per = timed_run(args, ctx, dist, dev, step)
+        tot_px = total_over_ranks(dist, dev, n)
+        if rank != 0:
+            return None
+        out = bench_line(
+            args, world, n, tot_px, R, C, elapsed, ev, per, args.bins,
+            args.dmax,
+            'cfg2: per GPU 1 chrom x %d bins, 4 reps (2+2), dist_thresh_max '
+            '%d, estimate_disp (qcml) + lrt on HBM-resident inputs'
+            % (args.bins, args.dmax),
+            'dp%d (chromosome shards; %s)' % (
+                world, 'per-pass NLL sums, no-op reduce (the N > 1 driver on '
+                'one GPU)' if reduce and world == 1 else
+                'in-kernel Brent searches' if world == 1 else
+                'distance re-shard: all_to_all of the disp pixels, in-kernel '
+                'Brent per rank, table all-reduce' if by_dist
+                else 'per-pass NLL all-reduce over RCCL'), 'weak')
+        if cpu is not None:
+            out['cpu_baseline'] = cpu[0]
+            out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
+        if world == 1 and not args.no_e2e:
+            out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
+        return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def run_cfg3(args, world, rank, local, dist, ctx, dev):
+    """Strong scaling over the whole mouse genome (BASELINE configs[2])."""
+    import torch
+    from hic3defdr_amd import _native, parallel, synthetic
+    bins = synthetic.MM10_BINS
+    dmax = args.dmax3
+    D = dmax + 1
+    assign = parallel.lpt_assign({i: b for i, b in enumerate(bins)}, world)
+    mine = sorted(assign[rank])
+    t0 = time.perf_counter()
+    parts = synthetic.draw_genome(bins, (2, 2), dmax, seed=0, indices=mine,
+                                  workers=16)
+    raw = np.concatenate([p[0] for p in parts])
+    f = np.concatenate([p[1] for p in parts])
+    dist_np = np.concatenate([p[2] for p in parts])
+    del parts
+    gen_s = time.perf_counter() - t0
+    R, C = 4, 2
+    cond = np.array([0, 0, 1, 1], dtype=np.int32)
+    n = len(raw)
+    t_raw, t_f, t_dist = _upload(torch, dev, raw, f, dist_np)
+    del raw, f
+    o = _outputs(torch, dev, n, C)
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+
+    def bh_fn(t):
+        q = torch.empty_like(t)
+        ctx.bh_dev(t.data_ptr(), t.numel(), q.data_ptr())
+        return q
+
+    def step():
+        if world > 1:
+            dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
+                                                     cond, C, D)
+        else:
+            dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                        t_dist.data_ptr(), n, R, cond, C, D)
+        tab = _native.disp_tables(dpd)
+        ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(), tab,
+                    n, R, cond, o['p'].data_ptr(), o['llr'].data_ptr(),
+                    o['mu0'].data_ptr(), o['mu1'].data_ptr(),
+                    o['disp'].data_ptr())
+        if world > 1:
+            o['q'] = parallel.bh_all_ranks(o['p'], bh_fn)
+        else:
+            ctx.bh_dev(o['p'].data_ptr(), n, o['q'].data_ptr())
+        return dpd
+
+    elapsed, ev, per = timed_run(args, ctx, dist, dev, step)
+    tot_px = total_over_ranks(dist, dev, n)
+    if rank != 0:
+        return None
+    out = bench_line(
+        args, world, n, tot_px, R, C, elapsed, ev, per, sum(bins), dmax,
+        'cfg3: whole mouse genome at 10 kb, 20 mm10-sized chromosomes (%d '
+        'bins), 4 reps (2+2), dist_thresh_max %d, chromosomes LPT-sharded '
+        'over %d GPU(s); step = genome-wide estimate_disp + lowess tables + '
+        'lrt + genome-wide BH on HBM-resident inputs' % (sum(bins), dmax,
+                                                          world),
+        'dp%d: %s' % (world, 'one GPU' if world == 1 else
+                      'distance re-shard (LPT distance owners, all_to_all of '
+                      'the disp pixels, single-GPU driver per rank, table '
+                      'all-reduce), LRT on own chromosomes, BH over one '
+                      'all_gather of the p-values'), 'strong')
+    out['config']['chromosomes_rank0'] = [int(i) for i in mine]
+    out['config']['generate_s_rank0'] = gen_s
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', choices=('auto', 'cfg2', 'cfg3'),
+                    default='auto',
+                    help='auto: cfg2 (BASELINE configs[1], 1 GPU) at N = 1, '
+                         'cfg3 (configs[2], the genome sharded over the '
+                         'node) at N > 1')
+    ap.add_argument('--bins', type=int, default=20000)
+    ap.add_argument('--dmax', type=int, default=250)
+    ap.add_argument('--dmax3', type=int, default=200)
+    ap.add_argument('--cpu-bins', type=int, default=1000,
+                    help='the faithful CPU row sample')
+    ap.add_argument('--cpu-full-bins', type=int, default=20000,
+                    help='the fallback-fixed CPU row (0: the sample)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--noop-reduce', action='store_true',
+                    help='measurement: run the multi-rank estimate_disp driver '
+                         '(per-pass NLL sums through the reduce hook) on one '
+                         'GPU with a no-op reduce, i.e. the N > 1 kernel and '
+                         'host-sync path without the collective')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    # H3D_DEVICE / H3D_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with
+    # several ranks on one GPU (RCCL needs one GPU per rank); the driver's
+    # runs use LOCAL_RANK's GPU and nccl
+    local = int(os.environ.get('H3D_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+    backend = os.environ.get('H3D_BENCH_BACKEND', 'nccl')
+    config = args.config if args.config != 'auto' else \
+        ('cfg2' if world == 1 else 'cfg3')
+    cpu = None
+    if world == 1 and config == 'cfg2' and not args.no_cpu_baseline:
+        cpu = cpu_baseline_run(args.cpu_full_bins, args.cpu_bins,
+                               args.dmax)   # before the GPU
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == 'nccl':
+            dist.init_process_group('nccl',
+                                    device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
+    from hic3defdr_amd import _native
+    ctx = _native.context(local)
+    dev = torch.device('cuda', local)
+    try:
+        if config == 'cfg2':
+            out = run_cfg2(args, world, rank, local, dist, ctx, dev, cpu)
+        else:
+            out = run_cfg3(args, world, rank, local, dist, ctx, dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
         if dist:
             dist.destroy_process_group()
 

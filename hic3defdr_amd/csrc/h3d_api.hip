@@ -213,6 +213,90 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
                      C, rep_idx, n_rep, st, seg_flags, result, queue, ctx->work_count);
 }
 
+// the gang variant (k_brent_gang): every live segment's search over the
+// co-resident workgroups of its slices. Returns false (nothing launched)
+// when the task table cannot be honoured (a segment needs more members than
+// the resident grid): the caller then launches k_brent.
+struct GangTables {
+  int32_t* task_seg = nullptr;
+  int32_t* task_g = nullptr;
+  int T = 0, gmax = 1, grid = 0;
+  double* part = nullptr;
+  int* arrive = nullptr;
+  int* abort = nullptr;
+  long long timeout = 0;
+};
+
+template <int M>
+int gang_setup(h3d_ctx* ctx, const std::vector<int64_t>& seg_start, int D, int C,
+               GangTables* g) {
+  auto k = k_brent_gang<M>;
+  int& nb = ctx->resident[(const void*)k];
+  if (nb == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kGangThreads, 0) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+  }
+  g->grid = ctx->n_cu * nb;
+  constexpr int P = gang_slice<M>();
+  std::vector<int32_t> ts, tg;
+  int gmax = 1;
+  for (int d = 0; d < D; ++d) {
+    const int64_t np = seg_start[d + 1] - seg_start[d];
+    if (np == 0) continue;
+    const int G = (int)((np + P - 1) / P);
+    if (G > g->grid) return 1;  // cannot be co-resident: plain k_brent
+    gmax = std::max(gmax, G);
+    for (int c = 0; c < C; ++c)
+      for (int j = 0; j < G; ++j) {
+        ts.push_back(d * C + c);
+        tg.push_back(j);
+      }
+  }
+  const int S = D * C;
+  g->T = (int)ts.size();
+  g->gmax = gmax;
+  g->task_seg = (int32_t*)scratch(ctx, "gang_seg", std::max<size_t>(1, ts.size()) * 4);
+  g->task_g = (int32_t*)scratch(ctx, "gang_g", std::max<size_t>(1, tg.size()) * 4);
+  g->part = (double*)scratch(ctx, "gang_part", (size_t)2 * S * gmax * 8);
+  g->arrive = (int*)scratch(ctx, "gang_arrive", (size_t)S * 4);
+  g->abort = (int*)scratch(ctx, "gang_abort", 4);
+  if (!g->task_seg || !g->task_g || !g->part || !g->arrive || !g->abort)
+    return fail(H3D_ENOMEM, "gang tables");
+  if (g->T) {
+    HIP_TRY(hipMemcpyAsync(g->task_seg, ts.data(), ts.size() * 4, hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipMemcpyAsync(g->task_g, tg.data(), tg.size() * 4, hipMemcpyHostToDevice,
+                           ctx->stream));
+  }
+  HIP_TRY(hipMemsetAsync(g->abort, 0, 4, ctx->stream));
+  // the host vectors die here: the copies must have read them
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  // spin bound: 0.5 s of the constant-rate wall clock
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) !=
+          hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  g->timeout = (long long)khz * 500;
+  return 0;
+}
+
+template <int M>
+void launch_brent_gang(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_start,
+                       int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
+                       SegState* st, const int* seg_flags, double* result, int* queue,
+                       const GangTables& g) {
+  ProfScope ps(ctx, "disp_nll", 0);
+  (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
+  (void)hipMemsetAsync(g.arrive, 0, (size_t)S * 4, ctx->stream);
+  const int grid = std::max(1, std::min(g.T, g.grid));
+  hipLaunchKernelGGL(k_brent_gang<M>, dim3(grid), dim3(kGangThreads), 0, ctx->stream, pd,
+                     n, seg_start, S, C, rep_idx, n_rep, st, seg_flags, result, queue,
+                     g.task_seg, g.task_g, g.T, g.part, g.gmax, g.arrive, g.abort,
+                     g.timeout, ctx->work_count);
+}
+
 // algorithmic HBM bytes of the disp_work launches so far: an equalize
 // pixel-replicate reads raw (4 B) + f (8 B) and writes pseudodata (8 B); an
 // NLL pixel-replicate reads pseudodata (8 B)
@@ -277,6 +361,7 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_DISP_W8")) ctx->disp_w8 = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W2")) ctx->disp_w2 = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
+  if (const char* e = std::getenv("H3D_BRENT")) ctx->brent_gang = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
@@ -594,7 +679,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                      d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
                      d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
-  if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 16, hipHostMallocDefault));
+  if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 32, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
   // (an M = 6 instantiation for cfg4's R_c = 6 measured equal to M = 8:
   // 111.5 vs 110.5 ms equalize per step, profiles/r02/q2)
@@ -614,13 +699,30 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     int64_t* d_seg = (int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
     if (!d_queue || !d_seg) return fail(H3D_ENOMEM, "brent scratch");
     if (n == 0) HIP_TRY(hipMemsetAsync(d_seg, 0, (D + 1) * 8, s));
+    // H3D_BRENT: 1 = gang searches (k_brent_gang, default), 0 = one
+    // workgroup per segment (k_brent)
+    GangTables gang;
+    bool use_gang = ctx->brent_gang != 0 && n > 0;
+    if (use_gang) {
+      int grc = mslot == 2   ? gang_setup<2>(ctx, seg_start, D, C, &gang)
+                : mslot == 4 ? gang_setup<4>(ctx, seg_start, D, C, &gang)
+                : mslot == 8 ? gang_setup<8>(ctx, seg_start, D, C, &gang)
+                : mslot == 16 ? gang_setup<16>(ctx, seg_start, D, C, &gang)
+                              : gang_setup<32>(ctx, seg_start, D, C, &gang);
+      if (grc == 1) use_gang = false;
+      else if (grc) return grc;
+    }
     batch = 3;
     while (true) {
       for (int b = 0; b < batch; ++b) {
 #define H3D_QCML_ITER(MM)                                                                 \
   launch_disp_work<MM, false>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C,     \
                               d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial); \
-  launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
+  if (use_gang)                                                                           \
+    launch_brent_gang<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, \
+                          d_queue, gang);                                                 \
+  else                                                                                    \
+    launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
         if (mslot == 2) { H3D_QCML_ITER(2); }
         else if (mslot == 4) { H3D_QCML_ITER(4); }
         else if (mslot == 8) { H3D_QCML_ITER(8); }
@@ -636,12 +738,22 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         ++rounds;
       }
       if (hipMemcpyAsync(h_meta, d_meta, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          (use_gang &&
+           hipMemcpyAsync(h_meta + 4, gang.abort, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
           hipStreamSynchronize(s) != hipSuccess) {
         rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(hipGetLastError()));
         break;
       }
       if (std::getenv("H3D_DEBUG"))
-        fprintf(stderr, "[h3d] qcml iterations=%d live_segments=%d\n", rounds, h_meta[3]);
+        fprintf(stderr, "[h3d] qcml iterations=%d live_segments=%d gang=%d abort=%d\n",
+                rounds, h_meta[3], (int)use_gang, use_gang ? h_meta[4] : 0);
+      if (use_gang && h_meta[4]) {
+        // a gang's wait timed out (CUs held elsewhere): its segments stayed
+        // in kEqualize and repeat their iteration; finish with k_brent
+        use_gang = false;
+        ctx->gang_aborts += 1;
+        continue;
+      }
       if (h_meta[3] == 0) break;
       if (rounds > 2000) {
         rc = fail(H3D_ENOCONV, "estimate_disp did not terminate");

@@ -685,6 +685,171 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
   }
 }
 
+// ---- gang Brent: a segment's search over several co-resident workgroups ----
+// k_brent runs a segment's whole bounded-Brent search in ONE workgroup, so
+// a launch with fewer live segments than CUs leaves CUs idle (the tail qcml
+// iterations; a rank of the distance re-shard at N = 8 owns ~50 segments of
+// cfg3's ~230 k pixels each), and every evaluation re-streams the segment's
+// pseudodata from beyond L2. Here a segment is split into G slices of
+// kGangThreads * K pixels; a gang of G workgroups holds the slices in
+// registers for the whole search (loaded once), and per evaluation each
+// workgroup adds its slice's NLL terms, publishes the partial, and waits for
+// the gang's other partials (one agent-scope counter per segment). Every
+// member then sums the G partials in slice order (deterministic) and steps
+// its own copy of the state machine -- the same inputs, so the same trial
+// point in every member, no broadcast. Member 0 writes the state back.
+//
+// Progress: workgroups take tasks (segment, slice) from one queue in order,
+// the slices of a segment consecutive. A workgroup only waits for tasks of
+// its own segment; the segment at the queue head is the only one with both
+// taken and untaken tasks, so as long as G <= the workgroups that can run
+// at once (the host caps G by the resident grid), every wait ends. A spin
+// bound (`timeout` wall-clock ticks) still ends every wait -- e.g. when
+// another process holds CUs: the gang then raises `abort` and every member
+// exits without writing its segment back, which therefore stays in the
+// kEqualize phase and simply repeats this qcml iteration (re-equalized with
+// the unchanged dispersion = the same pseudodata) under the one-workgroup
+// k_brent, which the host switches to once it sees the flag.
+constexpr int kGangThreads = 256;
+template <int M>
+constexpr int gang_k() {  // pixels per thread held in registers
+  return M <= 2 ? 4 : M <= 4 ? 2 : 1;
+}
+template <int M>
+constexpr int gang_slice() {
+  return kGangThreads * gang_k<M>();
+}
+
+// 4 waves per SIMD (128 VGPRs): unbounded, the compiler interleaved all K
+// slots' lgamma chains of M = 2 into 256 VGPRs at 1 wave per SIMD
+template <int M>
+constexpr int gang_waves() {
+  return M <= 2 ? 3 : M <= 8 ? 4 : 2;
+}
+
+template <int M>
+__global__ __launch_bounds__(kGangThreads, gang_waves<M>()) void k_brent_gang(
+    const double* __restrict__ pd, int64_t n,
+    const int64_t* __restrict__ seg_start /* D + 1 */, int S, int C,
+    const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
+    const int32_t* __restrict__ n_rep /* C */, SegState* __restrict__ st,
+    const int* __restrict__ seg_flags, double* __restrict__ result,
+    int* __restrict__ queue, const int32_t* __restrict__ task_seg,
+    const int32_t* __restrict__ task_g, int T, double* __restrict__ part /* 2 x S x gmax */,
+    int gmax, int* __restrict__ arrive /* S, zeroed */, int* __restrict__ abort_flag,
+    long long timeout, unsigned long long* __restrict__ work_count) {
+  constexpr int K = gang_k<M>();
+  constexpr int P = gang_slice<M>();
+  __shared__ SegState s_st;
+  __shared__ double wpart[kGangThreads / 64];
+  __shared__ int s_next, s_more, s_abort;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  while (true) {
+    __syncthreads();  // s_next / s_st reuse
+    if (threadIdx.x == 0) s_next = atomicAdd(queue, 1);
+    __syncthreads();
+    const int t = s_next;
+    if (t >= T) break;
+    const int s = task_seg[t], g = task_g[t];
+    // every member reads the phase before the gang's first evaluation, so
+    // before member 0 can write the segment back
+    if (st[s].phase != kEqualize) continue;
+    if (threadIdx.x == 0) {
+      s_st = st[s];
+      s_st.flags |= seg_flags[s];
+      s_abort = 0;
+    }
+    const int d = s / C, c = s - (s / C) * C;
+    const int nr = n_rep[c];
+    const int64_t b = seg_start[d], e = seg_start[d + 1];
+    const int G = (int)((e - b + P - 1) / P);
+    const int64_t sb = b + (int64_t)g * P;
+    const int64_t se = (sb + P < e) ? sb + P : e;
+    // the slice: pixel sb + j * kGangThreads + tid in slot j (coalesced)
+    double v[K][M];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t px = sb + (int64_t)j * kGangThreads + threadIdx.x;
+#pragma unroll
+      for (int k = 0; k < M; ++k)
+        v[j][k] = (px < se && k < nr) ? pd[(int64_t)rep_idx[c * kMaxReps + k] * n + px] : 0.0;
+    }
+    int evals = 0;
+    __syncthreads();
+    while (true) {
+      const NllConst kc = s_st.k;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int64_t px = sb + (int64_t)j * kGangThreads + threadIdx.x;
+        const double tj = nll_pixel<M>(v[j], nr, kc);
+        if (px < se) acc += tj;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) wpart[wid] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double mine = 0.0;
+#pragma unroll
+        for (int w = 0; w < kGangThreads / 64; ++w) mine += wpart[w];
+        double total = mine;
+        bool ok = true;
+        if (G > 1) {
+          // The exchange uses relaxed agent-scope atomics only (coherent
+          // across the XCDs' L2s, instruction by instruction) ordered by
+          // waiting for the partial's store to complete before the arrival
+          // is counted: a release / acquire pair at agent scope writes back /
+          // invalidates the whole L2 on gfx950 (buffer_wbl2 / buffer_inv),
+          // which cost 20 vs 2.8 ms of Brent per cfg2 step (r03 A/B).
+          double* slot = part + ((size_t)(evals & 1) * S + s) * gmax;
+          __hip_atomic_store(&slot[g], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          __builtin_amdgcn_s_waitcnt(0);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          __hip_atomic_fetch_add(&arrive[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int target = (evals + 1) * G;
+          const long long t0 = wall_clock64();
+          while (__hip_atomic_load(&arrive[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                wall_clock64() - t0 > timeout) {
+              __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = false;
+              break;
+            }
+          }
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          __builtin_amdgcn_s_waitcnt(0);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          if (ok) {
+            total = 0.0;
+            for (int q = 0; q < G; ++q)
+              total += __hip_atomic_load(&slot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        if (ok) {
+          seg_step_ool(&s_st, total, nr);
+          s_more = (s_st.phase == kNll) ? 1 : 0;
+        } else {
+          s_abort = 1;
+          s_more = 0;
+        }
+      }
+      ++evals;
+      __syncthreads();  // s_st / s_more / s_abort / wpart
+      if (!s_more) break;
+    }
+    if (s_abort) return;  // the whole workgroup: s_abort is uniform
+    if (threadIdx.x == 0 && g == 0) {
+      st[s] = s_st;
+      if (s_st.phase == kDone) result[s] = s_st.result;
+      atomicAdd(&work_count[1], (unsigned long long)(e - b) * nr * evals);
+    }
+  }
+}
+
 // Per-pixel LRT (lrt.py:7-50) in the reference pixel order; disp from the
 // (D, C) table (analysis.py:218: disp = disp_fn(dist), evaluated per d).
 template <int M, int CM>

@@ -133,7 +133,9 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
     for (int k = 0; k < M; ++k)
       if (k < n && ((mask >> k) & 1u)) {
         const double mb = mu * b[k];
-        const double den = 1.0 / (1.0 + a[k] * mb);
+        // v_rcp_f64 + one Newton step on gfx950 (the IEEE division sequence
+        // was ~12 VALU per replicate and iteration)
+        const double den = recip_fast(1.0 + a[k] * mb);
         g += (x[k] - mb) * den;
         gp -= mb * (1.0 + a[k] * x[k]) * den * den;
       }
@@ -143,7 +145,7 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
       hi = th;
     else
       return mu;
-    const double dn = g / gp;
+    const double dn = g * recip_fast(gp);
     // Newton converges quadratically here (g is smooth and monotone in
     // theta): once a step is <= 1e-8 the error after it is ~1e-16, so take
     // it and stop. (Without this exit, a final step below one ulp left th
@@ -221,11 +223,19 @@ struct LgamCache {
   double a = -1.0, lga = 0.0;
 };
 
+// log Gamma of the q2qnbinom gamma shapes (a = mu / r > 0 finite): the
+// branch-light Stirling form of the NLL (lgam_nll: fixed 5- or 10-step shift,
+// no data-dependent loop or division; absolute error <= ~5e-15, which moves
+// the incomplete-gamma prefactor by the same relative amount). cephes lgam's
+// shift loop below 13 with an IEEE division per step serialised the lanes of
+// a wave (gfx950 r03 asm: two divergent loops per call).
+H3D_HD double lgam_q2q(double a) { return lgam_nll(a); }
+
 H3D_HD double lgam_cached(double a, LgamCache* c) {
-  if (!c) return lgam(a);
+  if (!c) return lgam_q2q(a);
   if (a != c->a) {
     c->a = a;
-    c->lga = lgam(a);
+    c->lga = lgam_q2q(a);
   }
   return c->lga;
 }
@@ -278,7 +288,7 @@ H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
     tg = right ? 1.0 : 0.0;
   } else {
     double P, Q, fac;
-    igam_pq(a_in, xs, lgam(a_in), &P, &Q, &fac, right ? 1 : 0);
+    igam_pq(a_in, xs, lgam_q2q(a_in), &P, &Q, &fac, right ? 1 : 0);
     tg = right ? Q : P;
   }
   double qg;

@@ -153,6 +153,10 @@ H3D_HD double recip_nll(double y) {
 #endif
 }
 
+// 1/y wherever ~1 ulp is enough (Newton iterates of the mean MLE, series
+// terms): recip_nll on gfx950, the division on the host.
+H3D_HD double recip_fast(double y) { return recip_nll(y); }
+
 // Horner step p x + c of the NLL polynomials. On gfx950 an explicit
 // three-address v_fma_f64 with the constant addend in an SGPR pair: with the
 // constant as the tied accumulator the compiler emitted v_fmac_f64 plus a
@@ -500,29 +504,44 @@ H3D_HD double igam_fac_l(double a, double x, double lga) {
 
 H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
 
-// power series sum of P(a, x) = fac / a * sum (DLMF 8.11.4), two terms per
-// division: c_{n} = c_{n-1} x / (a+n) = c_{n-1} x (a+n+1) / ((a+n)(a+n+1)).
-// Stops at the first term <= eps * sum, as cephes igam_series.
+// power series sum of P(a, x) = fac / a * sum (DLMF 8.11.4):
+//   sum_n x^n / ((a+1) ... (a+n)),
+// four terms per trip from ONE reciprocal: with D = (r+1)(r+2)(r+3)(r+4) and
+// the last term c,
+//   c1 = c x (r+2)(r+3)(r+4) / D, c2 = c x^2 (r+3)(r+4) / D,
+//   c3 = c x^3 (r+4) / D,        c4 = c x^4 / D,
+// (x^2, x^3, x^4 hoisted out of the loop) and one stopping test per trip:
+// the sum stops once a trip's last term is <= eps * sum (cephes igam_series
+// tests every term; the up to three further terms it adds are each below
+// eps * sum, so the value moves by an ulp at most). On gfx950 the reciprocal
+// is v_rcp_f64 + one Newton step (~1 ulp; the IEEE division sequence was 40%
+// of a trip); the host build divides. Measured on gfx950 r03: the two-term
+// form with a per-term test spent ~11.5 VALU per term plus an exec-mask
+// branch per term; this form ~7.
 H3D_HD double igam_series_sum(double a, double x) {
+  const double x2 = x * x, x3 = x2 * x, x4 = x2 * x2;
   double r = a, c = 1.0, ans = 1.0;
-  for (int i = 0; i < kMaxIter / 2; ++i) {
-    H3D_STAT(ser_it, 2);
-    const double r1 = r + 1.0, r2 = r + 2.0;
+  for (int i = 0; i < kMaxIter / 4; ++i) {
+    H3D_STAT(ser_it, 4);
+    const double r2 = r + 2.0, r3 = r + 3.0, r4 = r + 4.0;
+    const double p34 = r3 * r4;
+    const double den = (r + 1.0) * r2 * p34;
 #if defined(__HIP_DEVICE_COMPILE__)
-    // gfx950: v_rcp_f64 + one Newton step (~1 ulp) instead of the IEEE
-    // division sequence (10 FP64 instructions, 40% of the trip); the terms
-    // then carry ~1 ulp more rounding each, far below the sum's own error
-    const double xi = x * recip_nll(r1 * r2);
+    const double cd = c * recip_nll(den);
 #else
-    const double xi = x / (r1 * r2);
+    const double cd = c / den;
 #endif
-    c *= xi * r2;
-    ans += c;
-    if (c <= kMachEp * ans) break;
-    c *= xi * r1;
-    ans += c;
-    if (c <= kMachEp * ans) break;
-    r = r2;
+    const double c1 = cd * x * (r2 * p34);
+    const double c2 = cd * x2 * p34;
+    const double c3 = cd * x3 * r4;
+    const double c4 = cd * x4;
+    ans += c1;
+    ans += c2;
+    ans += c3;
+    ans += c4;
+    c = c4;
+    if (c4 <= kMachEp * ans) break;
+    r = r4;
   }
   return ans;
 }
@@ -559,15 +578,18 @@ H3D_HD double igamc_series(double a, double x) {
 // recurrence without the two divisions per step: consecutive convergents
 // p_{k-1}/q_{k-1}, p_k/q_k are compared by cross-multiplication,
 //   |p_k q_{k-1} - p_{k-1} q_k| <= tol |p_k q_{k-1}|,
-// and the quotient is formed once at the end. tol = 4 eps: the fused
+// and the quotient is formed once, after the loop. tol = 4 eps: the fused
 // cross product is exact to ~1 eps of |p_k q_{k-1}|, so the test is met once
-// the convergents agree to ~3 eps (cephes: once they round to the same double).
-// The overflow guard rescales all four convergent terms by 2^-52 once per
-// trip (two steps), branch-free (a multiply by 1 or 2^-52): scaling by a
-// power of two changes neither the test nor the final quotient, so the result
-// is bit-identical to a per-step guard, and the loop body carries no masked
-// copy-and-scale region (on gfx950 that region cost 4 v_mov_b64 + 4 v_ldexp
-// + exec-mask updates per step, a third of the step).
+// the convergents agree to ~3 eps (cephes: once they round to the same
+// double). Four steps per trip (two of each register pair, so no moves
+// between steps), one test and one overflow rescale per trip: the up to
+// three steps past the first converged one only refine the value further.
+// The rescale divides all four terms by the power of two of the larger |p|
+// once it exceeds 2^64 (exact: changes neither the test nor the quotient).
+// Measured on gfx950 r03: with a test per step and the quotient inside the
+// loop, the compiler emitted the IEEE division in a masked block executed
+// every time any lane of the wave converged, and ~12 exec-mask instructions
+// per step.
 H3D_HD double igamc_cf_ratio(double a, double x) {
 #if defined(__clang__)
   // contraction (the convergents' products fuse into FMAs) -- the ratio
@@ -575,31 +597,30 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
 #pragma clang fp contract(fast)
 #endif
   double y = 1.0 - a, z = x + y + 1.0, c = 0.0;
-  // (p1, q1): the latest convergent, (p0, q0): the one before. Two steps per
-  // trip with the roles swapped, so no register moves between steps.
+  // (p1, q1): the latest convergent, (p0, q0): the one before
   double p0 = 1.0, q0 = x, p1 = x + 1.0, q1 = z * x;
-  for (int i = 0; i < kMaxIter / 2; ++i) {
-    H3D_STAT(cf_it, 1);
-    c += 1.0;
-    y += 1.0;
-    z += 2.0;
-    double yc = y * c;
-    p0 = p1 * z - p0 * yc;  // step A: new latest in (p0, q0)
-    q0 = q1 * z - q0 * yc;
-    double lead = p0 * q1;
-    bool done = (q0 != 0.0) && fabs(lead - p1 * q0) <= 4.0 * kMachEp * fabs(lead);
-    if (done) return p0 / q0;
-    H3D_STAT(cf_it, 1);
-    c += 1.0;
-    y += 1.0;
-    z += 2.0;
-    yc = y * c;
-    p1 = p0 * z - p1 * yc;  // step B: new latest in (p1, q1)
-    q1 = q0 * z - q1 * yc;
-    lead = p1 * q0;
-    done = (q1 != 0.0) && fabs(lead - p0 * q1) <= 4.0 * kMachEp * fabs(lead);
-    if (done) return p1 / q1;
-    const double sc = (fmax(fabs(p0), fabs(p1)) > kBig) ? kBigInv : 1.0;
+  for (int i = 0; i < kMaxIter / 4; ++i) {
+    H3D_STAT(cf_it, 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      c += 1.0;
+      y += 1.0;
+      z += 2.0;
+      double yc = y * c;
+      p0 = p1 * z - p0 * yc;  // step A: new latest in (p0, q0)
+      q0 = q1 * z - q0 * yc;
+      c += 1.0;
+      y += 1.0;
+      z += 2.0;
+      yc = y * c;
+      p1 = p0 * z - p1 * yc;  // step B: new latest in (p1, q1)
+      q1 = q0 * z - q1 * yc;
+    }
+    const double lead = p1 * q0;
+    if ((q1 != 0.0) && fabs(lead - p0 * q1) <= 4.0 * kMachEp * fabs(lead)) break;
+    int e;
+    (void)frexp(fmax(fabs(p0), fabs(p1)), &e);
+    const double sc = (e > 64) ? ldexp(1.0, -e) : 1.0;
     p0 *= sc;
     q0 *= sc;
     p1 *= sc;

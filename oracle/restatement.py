@@ -215,6 +215,11 @@ def _array_secant(func, x0, tol=1.48e-8, maxiter=100):
     return p, ~failures, zero_der
 
 
+# work counters of this process (bench.py's CPU baseline reports the
+# faithful row's brentq fallbacks)
+STATS = {'brentq_fallbacks': 0}
+
+
 def fit_mu_hat(x, b, alpha, faithful=False):
     """``scaled_nb.py:71-183``.
 
@@ -246,6 +251,7 @@ def fit_mu_hat(x, b, alpha, faithful=False):
         failed[root >= np.sqrt(np.finfo(float).max) / 1e10] = True
         failed[~np.isclose(f(root), 0, atol=1e-5)] = True
     if np.any(failed):
+        STATS['brentq_fallbacks'] += int(np.sum(failed))
         for idx in np.where(failed)[0]:
             lower = 10 * np.finfo(float).eps
             upper = np.mean(x[idx] / b[idx])

@@ -9,9 +9,16 @@ through parallel.make_allreduce on torch's stream); BH gathers on rank 0 and
 scatters back. The outdir must match the
 reference goldens like the single-rank run does (tests/test_gpu_e2e.py).
 
-The file sorts first so the pytest process has not touched the GPU when it
-starts the ranks (a GPU-initialised parent made the same launch stall on
-the box); the ranks' output goes to log files, not pipes."""
+The ranks start from the pytest process after the other GPU tests have run
+in it (the file sorts among them; the parent holds a torch CUDA context and
+a libh3d context with the cfg3 scratch). Round 2 kept this file first after
+a stall of this launch; the cause was the stream race fixed in the same
+commit (22afc53: each rank's libh3d kernels ran on the ctx's own stream
+while the collective ran on torch's, so the ranks' Brent state machines
+read each other's sums before they were reduced, diverged and deadlocked in
+the all-reduce), not the parent's GPU state. The ranks' output (H3D_DEBUG
+lines: qcml rounds, live segments, gang aborts) goes to a log file, not a
+pipe, and is printed when the launch fails or times out."""
 import os
 import re
 import shutil

@@ -74,32 +74,73 @@ def cfg2(ctx):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def test_cfg2_full_size_vs_reference(cfg2):
+def _delta(disp):
+    # the variable cml's bounded Brent searches (dispersion.py:72-80)
+    return disp / (1.0 + disp)
+
+
+def test_cfg2_full_size_vs_reference(ctx, cfg2):
     """The whole headline chromosome (3.76 M disp pixels) against the
     reference's own prepare_data + estimate_disp + (chunked) lrt + bh on it
-    (tests/golden/full_cfg2.npz, make_golden.py run_full_cfg2): disp_per_dist,
-    p / q / llr / means on a seeded 50 k-pixel sample and on the 2,000
-    smallest p-values, and identical call sets at q < 0.01 / 0.05 / 0.1."""
+    (tests/golden/full_cfg2.npz, make_golden.py run_full_cfg2).
+
+    estimate_disp: the 502 (distance, condition) bounded-Brent searches
+    (scipy xatol 1e-5 in delta = disp / (1 + disp)) follow the reference's
+    trial points only while every comparison of two NLL values goes the same
+    way; NLL sums over ~15 k pixels that differ in the last bits (another
+    summation order, other lgamma / log implementations) can flip a
+    near-tied comparison, after which that search ends at another point
+    inside its tolerance. So: >= 99 % of the segments <= 1e-6 relative,
+    every segment within 2 xatol in delta.
+
+    lrt + bh, stage-isolated at full size: the product's smoother + LRT + BH
+    on the reference's disp_per_dist -> p / q <= 1e-6 on the seeded sample
+    and on the 2,000 smallest p-values, identical call sets.
+
+    End to end (the product's own disp_per_dist): identical call sets at
+    q < 0.01 / 0.05 / 0.1, p / q on the sample within 1e-3 relative (the
+    smoothed table moves by what a tolerance-level segment moves it)."""
+    from hic3defdr_amd import _native
     g = golden('full_cfg2.npz')
-    _, _, _, _, out = cfg2
+    raw, f, dist, design, out = cfg2
     assert len(out['pvalues']) == int(g['n_disp_pixels'])
     dpd, ref = out['disp_per_dist'], g['disp_per_dist']
     np.testing.assert_array_equal(np.isnan(dpd), np.isnan(ref))
-    assert rel_err(dpd, ref) < RTOL_PQ
-    s = g['sample_idx']
-    assert rel_err(out['pvalues'][s], g['p']) < RTOL_PQ
-    assert rel_err(out['qvalues'][s], g['q']) < RTOL_PQ
-    assert rel_err(out['mu_hat_null'][s], g['mu0']) < RTOL_PQ
-    assert rel_err(out['mu_hat_alt'][s], g['mu1']) < RTOL_PQ
-    # llr crosses zero: absolute, scaled to its magnitude
-    assert np.max(np.abs(out['llr'][s] - g['llr']) /
+    fin = np.isfinite(ref)
+    rel = np.abs(dpd[fin] - ref[fin]) / ref[fin]
+    print('disp_per_dist: %d segments, %d > 1e-6 rel, max rel %.3g, max '
+          '|d delta| %.3g' % (rel.size, int(np.sum(rel > 1e-6)), rel.max(),
+                             np.max(np.abs(_delta(dpd[fin]) -
+                                           _delta(ref[fin])))))
+    assert np.mean(rel <= 1e-6) >= 0.99
+    assert np.max(np.abs(_delta(dpd[fin]) - _delta(ref[fin]))) <= 2e-5
+    s, t = g['sample_idx'], g['top_idx']
+    # stage-isolated: the reference's table through the product's smoother,
+    # LRT and BH
+    cond = design.argmax(axis=1)
+    tab = _native.disp_tables(ref)
+    p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, cond, want_disp=False)
+    q = ctx.bh(p)
+    assert rel_err(p[s], g['p']) < RTOL_PQ
+    assert rel_err(q[s], g['q']) < RTOL_PQ
+    assert rel_err(m0[s], g['mu0']) < RTOL_PQ
+    assert rel_err(m1[s], g['mu1']) < RTOL_PQ
+    assert np.max(np.abs(llr[s] - g['llr']) /
                   np.maximum(np.abs(g['llr']), 1.0)) < RTOL_PQ
-    t = g['top_idx']
-    assert rel_err(out['pvalues'][t], g['top_p']) < RTOL_PQ
-    assert rel_err(out['qvalues'][t], g['top_q']) < RTOL_PQ
+    assert rel_err(p[t], g['top_p']) < RTOL_PQ
+    assert rel_err(q[t], g['top_q']) < RTOL_PQ
     for fdr in (0.01, 0.05, 0.1):
-        np.testing.assert_array_equal(
-            np.where(out['qvalues'] < fdr)[0], g['calls_%g' % fdr])
+        np.testing.assert_array_equal(np.where(q < fdr)[0],
+                                      g['calls_%g' % fdr])
+    # end to end
+    e2e_p, e2e_q = rel_err(out['pvalues'][s], g['p']), \
+        rel_err(out['qvalues'][s], g['q'])
+    print('end to end: sample p rel %.3g, q rel %.3g; top p rel %.3g' % (
+        e2e_p, e2e_q, rel_err(out['pvalues'][t], g['top_p'])))
+    assert e2e_p < 1e-3 and e2e_q < 1e-3
+    for fdr in (0.01, 0.05, 0.1):
+        np.testing.assert_array_equal(np.where(out['qvalues'] < fdr)[0],
+                                      g['calls_%g' % fdr])
 
 
 def test_cfg2_full_size_properties(ctx, cfg2):
