@@ -545,11 +545,28 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
     bins = synthetic.MM10_BINS
     dmax = args.dmax3
     D = dmax + 1
-    assign = parallel.lpt_assign({i: b for i, b in enumerate(bins)}, world)
-    mine = sorted(assign[rank])
+    # H3D_BENCH_EMULATE=r/N (N = 1 only): time rank r's share of an N-GPU
+    # run on this one GPU -- estimate_disp over the distances the LPT owner
+    # table gives rank r (what it holds after the all_to_all), lrt + BH over
+    # the chromosomes LPT gives it; the collectives are not run
+    emu = os.environ.get('H3D_BENCH_EMULATE') if world == 1 else None
+    e_rank, e_world = (int(v) for v in emu.split('/')) if emu else (rank, world)
+    assign = parallel.lpt_assign({i: b for i, b in enumerate(bins)}, e_world)
+    mine = sorted(assign[e_rank])
     t0 = time.perf_counter()
-    parts = synthetic.draw_genome(bins, (2, 2), dmax, seed=0, indices=mine,
-                                  workers=16)
+    parts = synthetic.draw_genome(bins, (2, 2), dmax, seed=0,
+                                  indices=None if emu else mine, workers=16)
+    if emu:
+        own = [p for i, p in enumerate(parts) if i in mine]
+        d_all = np.concatenate([p[2] for p in parts])
+        owner = parallel.distance_owners(
+            np.bincount(d_all, minlength=D)[:D], e_world)
+        keep = owner[d_all] == e_rank
+        e_raw = np.concatenate([p[0] for p in parts])[keep]
+        e_f = np.concatenate([p[1] for p in parts])[keep]
+        e_dist = d_all[keep]
+        del d_all
+        parts = own
     raw = np.concatenate([p[0] for p in parts])
     f = np.concatenate([p[1] for p in parts])
     dist_np = np.concatenate([p[2] for p in parts])
@@ -560,6 +577,10 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
     n = len(raw)
     t_raw, t_f, t_dist = _upload(torch, dev, raw, f, dist_np)
     del raw, f
+    if emu:
+        e_n = len(e_raw)
+        te_raw, te_f, te_dist = _upload(torch, dev, e_raw, e_f, e_dist)
+        del e_raw, e_f
     o = _outputs(torch, dev, n, C)
     torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)
@@ -575,6 +596,10 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
         if world > 1:
             dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
                                                      cond, C, D)
+        elif emu:
+            dpd = ctx.disp_per_dist_dev(te_raw.data_ptr(), te_f.data_ptr(),
+                                        te_dist.data_ptr(), e_n, R, cond, C, D)
+            dpd[np.isnan(dpd)] = 0.05   # other ranks' rows (not run here)
         else:
             dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                         t_dist.data_ptr(), n, R, cond, C, D)
@@ -607,6 +632,14 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
                       'all_gather of the p-values'), 'strong')
     out['config']['chromosomes_rank0'] = [int(i) for i in mine]
     out['config']['generate_s_rank0'] = gen_s
+    if emu:
+        out['emulated'] = {
+            'rank': e_rank, 'of': e_world, 'disp_pixels_estimate_disp': e_n,
+            'note': 'one rank\'s share of an N-GPU cfg3 run, timed alone on '
+                    'one GPU: estimate_disp over its LPT-owned distances, lrt '
+                    '+ BH over its LPT-owned chromosomes; no collectives (the '
+                    'all_to_all, table all-reduce and p all_gather are not '
+                    'run). value = its pixels / time, NOT a scaling number'}
     return out
 
 

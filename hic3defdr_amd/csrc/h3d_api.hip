@@ -214,19 +214,21 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
 }
 
 // the gang variant (k_brent_gang): every live segment's search over the
-// co-resident workgroups of its slices. Returns false (nothing launched)
-// when the task table cannot be honoured (a segment needs more members than
-// the resident grid): the caller then launches k_brent.
+// co-resident workgroups of its slices.
 struct GangTables {
   int32_t* task_seg = nullptr;
   int32_t* task_g = nullptr;
   int T = 0, gmax = 1, grid = 0;
+  int64_t P = 0;
   double* part = nullptr;
-  int* arrive = nullptr;
+  int* tag = nullptr;
   int* abort = nullptr;
   long long timeout = 0;
 };
 
+// Returns 1 (nothing set up) when one workgroup per segment already fills
+// the chip -- the gang's exchange only pays where CUs would idle -- or when
+// a gang would not fit the resident grid.
 template <int M>
 int gang_setup(h3d_ctx* ctx, const std::vector<int64_t>& seg_start, int D, int C,
                GangTables* g) {
@@ -238,7 +240,20 @@ int gang_setup(h3d_ctx* ctx, const std::vector<int64_t>& seg_start, int D, int C
       nb = 1;
   }
   g->grid = ctx->n_cu * nb;
-  constexpr int P = gang_slice<M>();
+  int live = 0;
+  int64_t total = 0;
+  for (int d = 0; d < D; ++d) {
+    const int64_t np = seg_start[d + 1] - seg_start[d];
+    if (np) live += C;
+    total += np * C;
+  }
+  // H3D_BRENT=1 (auto): gangs when the segments leave CUs without a
+  // workgroup; 2: always
+  if (ctx->brent_gang == 1 && live >= ctx->n_cu) return 1;
+  // slices: about two resident grids of them over the whole call, at least
+  // 1024 pixels (4 per thread)
+  int64_t P = (total + 2 * (int64_t)g->grid - 1) / (2 * (int64_t)g->grid);
+  P = std::max<int64_t>(1024, (P + kGangThreads - 1) / kGangThreads * kGangThreads);
   std::vector<int32_t> ts, tg;
   int gmax = 1;
   for (int d = 0; d < D; ++d) {
@@ -256,12 +271,13 @@ int gang_setup(h3d_ctx* ctx, const std::vector<int64_t>& seg_start, int D, int C
   const int S = D * C;
   g->T = (int)ts.size();
   g->gmax = gmax;
+  g->P = P;
   g->task_seg = (int32_t*)scratch(ctx, "gang_seg", std::max<size_t>(1, ts.size()) * 4);
   g->task_g = (int32_t*)scratch(ctx, "gang_g", std::max<size_t>(1, tg.size()) * 4);
   g->part = (double*)scratch(ctx, "gang_part", (size_t)2 * S * gmax * 8);
-  g->arrive = (int*)scratch(ctx, "gang_arrive", (size_t)S * 4);
+  g->tag = (int*)scratch(ctx, "gang_tag", (size_t)2 * S * gmax * 4);
   g->abort = (int*)scratch(ctx, "gang_abort", 4);
-  if (!g->task_seg || !g->task_g || !g->part || !g->arrive || !g->abort)
+  if (!g->task_seg || !g->task_g || !g->part || !g->tag || !g->abort)
     return fail(H3D_ENOMEM, "gang tables");
   if (g->T) {
     HIP_TRY(hipMemcpyAsync(g->task_seg, ts.data(), ts.size() * 4, hipMemcpyHostToDevice,
@@ -289,11 +305,11 @@ void launch_brent_gang(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t*
                        const GangTables& g) {
   ProfScope ps(ctx, "disp_nll", 0);
   (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
-  (void)hipMemsetAsync(g.arrive, 0, (size_t)S * 4, ctx->stream);
+  (void)hipMemsetAsync(g.tag, 0, (size_t)2 * S * g.gmax * 4, ctx->stream);
   const int grid = std::max(1, std::min(g.T, g.grid));
   hipLaunchKernelGGL(k_brent_gang<M>, dim3(grid), dim3(kGangThreads), 0, ctx->stream, pd,
                      n, seg_start, S, C, rep_idx, n_rep, st, seg_flags, result, queue,
-                     g.task_seg, g.task_g, g.T, g.part, g.gmax, g.arrive, g.abort,
+                     g.task_seg, g.task_g, g.T, g.P, g.part, g.tag, g.gmax, g.abort,
                      g.timeout, ctx->work_count);
 }
 
@@ -699,8 +715,9 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     int64_t* d_seg = (int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
     if (!d_queue || !d_seg) return fail(H3D_ENOMEM, "brent scratch");
     if (n == 0) HIP_TRY(hipMemsetAsync(d_seg, 0, (D + 1) * 8, s));
-    // H3D_BRENT: 1 = gang searches (k_brent_gang, default), 0 = one
-    // workgroup per segment (k_brent)
+    // H3D_BRENT: 1 (default) = gang searches (k_brent_gang) when the
+    // segments are fewer than the CUs, 2 = always, 0 = one workgroup per
+    // segment (k_brent)
     GangTables gang;
     bool use_gang = ctx->brent_gang != 0 && n > 0;
     if (use_gang) {

@@ -94,7 +94,8 @@ struct h3d_ctx {
   // k_brent<2> (3.5 vs 3.9 ms), equalize is unchanged (same VGPR profile)
   int disp_w2 = 4;
   int disp_m2 = 1;
-  // H3D_BRENT: 1 = gang Brent searches (k_brent_gang), 0 = k_brent
+  // H3D_BRENT: 1 = gang Brent searches (k_brent_gang) where one workgroup
+  // per segment leaves CUs idle, 2 = always, 0 = k_brent only
   int brent_gang = 1;
   int gang_aborts = 0;  // gang waits that timed out (fell back to k_brent)
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8

@@ -686,18 +686,27 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
 }
 
 // ---- gang Brent: a segment's search over several co-resident workgroups ----
-// k_brent runs a segment's whole bounded-Brent search in ONE workgroup, so
-// a launch with fewer live segments than CUs leaves CUs idle (the tail qcml
-// iterations; a rank of the distance re-shard at N = 8 owns ~50 segments of
-// cfg3's ~230 k pixels each), and every evaluation re-streams the segment's
-// pseudodata from beyond L2. Here a segment is split into G slices of
-// kGangThreads * K pixels; a gang of G workgroups holds the slices in
-// registers for the whole search (loaded once), and per evaluation each
-// workgroup adds its slice's NLL terms, publishes the partial, and waits for
-// the gang's other partials (one agent-scope counter per segment). Every
-// member then sums the G partials in slice order (deterministic) and steps
-// its own copy of the state machine -- the same inputs, so the same trial
-// point in every member, no broadcast. Member 0 writes the state back.
+// k_brent runs a segment's whole bounded-Brent search in ONE workgroup, so a
+// call with fewer segments than CUs leaves CUs idle: a rank of the distance
+// re-shard at N = 8 owns ~50 of cfg3's segments of ~230 k pixels each, and
+// its k_brent ran on 50 CUs. Here a segment of n pixels is split into G
+// slices of P pixels (the host sizes P so the whole call has about two
+// resident grids of slices); a gang of G workgroups each adds its slice's
+// NLL terms per evaluation, publishes the partial, and waits for the gang's
+// other partials. Every member then sums the G partials in slice order
+// (deterministic) and steps its own copy of the state machine -- the same
+// inputs, so the same trial point in every member, no broadcast. Member 0
+// writes the state back.
+//
+// Exchange: per (segment, slice, evaluation parity) a partial and a tag
+// (evaluation + 1), written with relaxed agent-scope stores (coherent across
+// the XCDs' L2s instruction by instruction), the tag only after the partial's
+// store has completed; the readers (the lanes of wave 0, one slice each)
+// poll the tags, then load the partials -- one vector load per 64 slices. A
+// release / acquire pair at agent scope writes back / invalidates the whole
+// L2 on gfx950 (buffer_wbl2 / buffer_inv), and a single arrival counter with
+// partials read one by one cost ~20 us per evaluation (r03 A/B: 13.3 vs
+// 2.8 ms of Brent per cfg2 step).
 //
 // Progress: workgroups take tasks (segment, slice) from one queue in order,
 // the slices of a segment consecutive. A workgroup only waits for tasks of
@@ -711,35 +720,19 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
 // the unchanged dispersion = the same pseudodata) under the one-workgroup
 // k_brent, which the host switches to once it sees the flag.
 constexpr int kGangThreads = 256;
-template <int M>
-constexpr int gang_k() {  // pixels per thread held in registers
-  return M <= 2 ? 4 : M <= 4 ? 2 : 1;
-}
-template <int M>
-constexpr int gang_slice() {
-  return kGangThreads * gang_k<M>();
-}
-
-// 4 waves per SIMD (128 VGPRs): unbounded, the compiler interleaved all K
-// slots' lgamma chains of M = 2 into 256 VGPRs at 1 wave per SIMD
-template <int M>
-constexpr int gang_waves() {
-  return M <= 2 ? 3 : M <= 8 ? 4 : 2;
-}
 
 template <int M>
-__global__ __launch_bounds__(kGangThreads, gang_waves<M>()) void k_brent_gang(
+__global__ __launch_bounds__(kGangThreads) void k_brent_gang(
     const double* __restrict__ pd, int64_t n,
     const int64_t* __restrict__ seg_start /* D + 1 */, int S, int C,
     const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
     const int32_t* __restrict__ n_rep /* C */, SegState* __restrict__ st,
     const int* __restrict__ seg_flags, double* __restrict__ result,
     int* __restrict__ queue, const int32_t* __restrict__ task_seg,
-    const int32_t* __restrict__ task_g, int T, double* __restrict__ part /* 2 x S x gmax */,
-    int gmax, int* __restrict__ arrive /* S, zeroed */, int* __restrict__ abort_flag,
-    long long timeout, unsigned long long* __restrict__ work_count) {
-  constexpr int K = gang_k<M>();
-  constexpr int P = gang_slice<M>();
+    const int32_t* __restrict__ task_g, int T, int64_t P,
+    double* __restrict__ part /* 2 x S x gmax */, int* __restrict__ tag /* 2 x S x gmax, zeroed */,
+    int gmax, int* __restrict__ abort_flag, long long timeout,
+    unsigned long long* __restrict__ work_count) {
   __shared__ SegState s_st;
   __shared__ double wpart[kGangThreads / 64];
   __shared__ int s_next, s_more, s_abort;
@@ -765,57 +758,69 @@ __global__ __launch_bounds__(kGangThreads, gang_waves<M>()) void k_brent_gang(
     const int G = (int)((e - b + P - 1) / P);
     const int64_t sb = b + (int64_t)g * P;
     const int64_t se = (sb + P < e) ? sb + P : e;
-    // the slice: pixel sb + j * kGangThreads + tid in slot j (coalesced)
-    double v[K][M];
+    int ri[M];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const int64_t px = sb + (int64_t)j * kGangThreads + threadIdx.x;
-#pragma unroll
-      for (int k = 0; k < M; ++k)
-        v[j][k] = (px < se && k < nr) ? pd[(int64_t)rep_idx[c * kMaxReps + k] * n + px] : 0.0;
-    }
+    for (int k = 0; k < M; ++k) ri[k] = (k < nr) ? rep_idx[c * kMaxReps + k] : 0;
     int evals = 0;
     __syncthreads();
     while (true) {
       const NllConst kc = s_st.k;
       double acc = 0.0;
+      // the slice, two pixels per trip for M <= 4 (independent lgamma
+      // chains), as k_brent
+      constexpr int kPair = M <= 4 ? 2 : 1;
+      for (int64_t px = sb + threadIdx.x; px < se; px += kPair * kGangThreads) {
+        const int64_t qx = px + kGangThreads;
+        const bool two = kPair == 2 && qx < se;
+        double v[M], w[M];
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int64_t px = sb + (int64_t)j * kGangThreads + threadIdx.x;
-        const double tj = nll_pixel<M>(v[j], nr, kc);
-        if (px < se) acc += tj;
+        for (int k = 0; k < M; ++k) {
+          v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
+          w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
+        }
+        acc += nll_pixel<M>(v, nr, kc);
+        if constexpr (kPair == 2) {
+          const double t1 = nll_pixel<M>(w, nr, kc);
+          if (two) acc += t1;
+        }
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) wpart[wid] = acc;
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (wid == 0) {
         double mine = 0.0;
 #pragma unroll
         for (int w = 0; w < kGangThreads / 64; ++w) mine += wpart[w];
         double total = mine;
         bool ok = true;
         if (G > 1) {
-          // The exchange uses relaxed agent-scope atomics only (coherent
-          // across the XCDs' L2s, instruction by instruction) ordered by
-          // waiting for the partial's store to complete before the arrival
-          // is counted: a release / acquire pair at agent scope writes back /
-          // invalidates the whole L2 on gfx950 (buffer_wbl2 / buffer_inv),
-          // which cost 20 vs 2.8 ms of Brent per cfg2 step (r03 A/B).
-          double* slot = part + ((size_t)(evals & 1) * S + s) * gmax;
-          __hip_atomic_store(&slot[g], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          __builtin_amdgcn_s_waitcnt(0);
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          __hip_atomic_fetch_add(&arrive[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int target = (evals + 1) * G;
+          const size_t base = ((size_t)(evals & 1) * S + s) * gmax;
+          const int want = evals + 1;
+          if (lane == 0) {
+            __hip_atomic_store(&part[base + g], mine, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __hip_atomic_store(&tag[base + g], want, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+          // wave 0 polls the G tags, lane q the slices q, q + 64, ...
           const long long t0 = wall_clock64();
-          while (__hip_atomic_load(&arrive[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                 target) {
+          while (true) {
+            bool mine_ready = true;
+            for (int q = lane; q < G; q += 64)
+              mine_ready &= __hip_atomic_load(&tag[base + q], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) == want;
+            if (__all(mine_ready)) break;
             __builtin_amdgcn_s_sleep(1);
-            if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                wall_clock64() - t0 > timeout) {
-              __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool stop =
+                __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                wall_clock64() - t0 > timeout;
+            if (stop) {
+              if (lane == 0)
+                __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               ok = false;
               break;
             }
@@ -824,17 +829,23 @@ __global__ __launch_bounds__(kGangThreads, gang_waves<M>()) void k_brent_gang(
           __builtin_amdgcn_s_waitcnt(0);
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
           if (ok) {
-            total = 0.0;
-            for (int q = 0; q < G; ++q)
-              total += __hip_atomic_load(&slot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double sum = 0.0;
+            for (int q = lane; q < G; q += 64)
+              sum += __hip_atomic_load(&part[base + q], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+            total = sum;  // the same fixed tree in every member
           }
         }
-        if (ok) {
-          seg_step_ool(&s_st, total, nr);
-          s_more = (s_st.phase == kNll) ? 1 : 0;
-        } else {
-          s_abort = 1;
-          s_more = 0;
+        if (lane == 0) {
+          if (ok) {
+            seg_step_ool(&s_st, total, nr);
+            s_more = (s_st.phase == kNll) ? 1 : 0;
+          } else {
+            s_abort = 1;
+            s_more = 0;
+          }
         }
       }
       ++evals;

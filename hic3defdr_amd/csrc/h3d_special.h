@@ -156,6 +156,15 @@ H3D_HD double recip_nll(double y) {
 // 1/y wherever ~1 ulp is enough (Newton iterates of the mean MLE, series
 // terms): recip_nll on gfx950, the division on the host.
 H3D_HD double recip_fast(double y) { return recip_nll(y); }
+// a / b to ~1 ulp by recip_fast (the equalize pass's quantile-map and
+// Halley-step quotients, whose rounding is far below their tests' bars)
+H3D_HD double div_fast(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return a * recip_nll(b);
+#else
+  return a / b;
+#endif
+}
 
 // Horner step p x + c of the NLL polynomials. On gfx950 an explicit
 // three-address v_fma_f64 with the constant addend in an SGPR pair: with the
@@ -357,6 +366,40 @@ H3D_HD double stirling_nll(double r2) {
   return hfma(q, r2, 1.0 / 12.0);
 }
 
+// e^x on gfx950, straight-line: x = k ln2 + r (|r| <= ln2 / 2, Cody-Waite
+// with fdlibm's split ln2), e^r by its degree-13 Taylor polynomial
+// (truncation < 5e-18 relative) in hfma steps with the coefficients in
+// SGPRs, scaled by ldexp; overflow / underflow / NaN as libm. ~1 ulp. OCML's
+// exp carried a v_mov_b64 copy of its constant per Horner step. Host: exp.
+H3D_HD double exp_fast(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double kd = rint(x * 1.44269504088896338700e+00);
+  double r = fma(kd, -6.93147180369123816490e-01, x);
+  r = fma(kd, -1.90821492927058770002e-10, r);
+  double p = 1.0 / 6227020800.0;              // 1/13!
+  p = hfma(p, r, 1.0 / 479001600.0);
+  p = hfma(p, r, 1.0 / 39916800.0);
+  p = hfma(p, r, 1.0 / 3628800.0);
+  p = hfma(p, r, 1.0 / 362880.0);
+  p = hfma(p, r, 1.0 / 40320.0);
+  p = hfma(p, r, 1.0 / 5040.0);
+  p = hfma(p, r, 1.0 / 720.0);
+  p = hfma(p, r, 1.0 / 120.0);
+  p = hfma(p, r, 1.0 / 24.0);
+  p = hfma(p, r, 1.0 / 6.0);
+  p = hfma(p, r, 0.5);
+  p = hfma(p, r, 1.0);
+  p = hfma(p, r, 1.0);
+  const int k = (int)fmax(fmin(kd, 1100.0), -1100.0);
+  double v = ldexp(p, k);
+  v = (x > 7.09782712893383996843e2) ? INFINITY : v;
+  v = (x < -7.45133219101941108420e2) ? 0.0 : v;
+  return (x != x) ? x : v;
+#else
+  return exp(x);
+#endif
+}
+
 // degree-5 rising factorial x (x+1) (x+2) (x+3) (x+4)
 H3D_HD double rise5(double x) {
   return hfma(hfma(hfma(x + 10.0, x, 35.0), x, 50.0), x, 24.0) * x;
@@ -491,15 +534,17 @@ H3D_HD double stirling_corr(double a) {
 }
 
 // x^a e^-x / Gamma(a), given lga = lgam(a).
+// (table-driven log_fast / straight-line exp_fast: the exponent's own
+// conditioning, a few ulp of |a ln x|, dominates their <= 1 ulp)
 H3D_HD double igam_fac_l(double a, double x, double lga) {
   if (fabs(a - x) > 0.4 * fabs(a) || a < 10.0) {
-    double ax = a * log(x) - x - lga;
+    double ax = a * log_fast(x) - x - lga;
     if (ax < -kMaxLog) return 0.0;
-    return exp(ax);
+    return exp_fast(ax);
   }
   H3D_STAT(fac_l1, 1);
   double s = (x - a) / a;
-  return exp(a * log1pmx(s) + 0.5 * log(a / kTwoPi) - stirling_corr(a));
+  return exp_fast(a * log1pmx(s) + 0.5 * log_fast(a / kTwoPi) - stirling_corr(a));
 }
 
 H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
@@ -584,8 +629,10 @@ H3D_HD double igamc_series(double a, double x) {
 // double). Four steps per trip (two of each register pair, so no moves
 // between steps), one test and one overflow rescale per trip: the up to
 // three steps past the first converged one only refine the value further.
-// The rescale divides all four terms by the power of two of the larger |p|
-// once it exceeds 2^64 (exact: changes neither the test nor the quotient).
+// The rescale multiplies all four terms by 2^-64 once |p| exceeds 2^64
+// (exact: changes neither the test nor the quotient; |p0| ~ |p1|, and four
+// steps grow them by ~z^4, far inside the double range for the q2qnbinom
+// arguments).
 // Measured on gfx950 r03: with a test per step and the quotient inside the
 // loop, the compiler emitted the IEEE division in a masked block executed
 // every time any lane of the wave converged, and ~12 exec-mask instructions
@@ -618,9 +665,7 @@ H3D_HD double igamc_cf_ratio(double a, double x) {
     }
     const double lead = p1 * q0;
     if ((q1 != 0.0) && fabs(lead - p0 * q1) <= 4.0 * kMachEp * fabs(lead)) break;
-    int e;
-    (void)frexp(fmax(fabs(p0), fabs(p1)), &e);
-    const double sc = (e > 64) ? ldexp(1.0, -e) : 1.0;
+    const double sc = (fabs(p1) > 0x1p64) ? 0x1p-64 : 1.0;
     p0 *= sc;
     q0 *= sc;
     p1 *= sc;
@@ -1000,16 +1045,18 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
       igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
       if (fac == 0.0) return x;
       F = (upper ? Q : P) - t;
-      dP = fac / x;
+      dP = div_fast(fac, x);
       xe = x;
       Fe = F;
       dPe = dP;
     }
     // Newton ratio f / f' (f' = -P' on the upper tail), Halley correction
-    const double f_fp = upper ? -F / dP : F / dP;
-    const double fpp_fp = -1.0 + (a - 1) / x;
+    // (quotients to ~1 ulp: a Halley step's rounding does not reach the
+    // root it converges to)
+    const double f_fp = div_fast(upper ? -F : F, dP);
+    const double fpp_fp = -1.0 + div_fast(a - 1, x);
     double xn = is_inf(fpp_fp) ? x - f_fp
-                               : x - f_fp / (1.0 - 0.5 * f_fp * fpp_fp);
+                               : x - div_fast(f_fp, 1.0 - 0.5 * f_fp * fpp_fp);
     if (!(xn > 0.0)) xn = 0.5 * x;  // safeguard: stay in the support
     const double dx = fabs(xn - x);
     x = xn;

@@ -16,9 +16,11 @@ a stall of this launch; the cause was the stream race fixed in the same
 commit (22afc53: each rank's libh3d kernels ran on the ctx's own stream
 while the collective ran on torch's, so the ranks' Brent state machines
 read each other's sums before they were reduced, diverged and deadlocked in
-the all-reduce), not the parent's GPU state. The ranks' output (H3D_DEBUG
-lines: qcml rounds, live segments, gang aborts) goes to a log file, not a
-pipe, and is printed when the launch fails or times out."""
+the all-reduce), not the parent's GPU state: round 3 runs this file after
+test_alternatives, test_gpu_cfg3 and test_gpu_e2e in the same pytest
+process (profiles/r03/gpu_tests_r03c.log), both modes green. The ranks'
+output (H3D_DEBUG lines: qcml rounds, live segments, gang aborts) goes to a
+log file, not a pipe, and is printed when the launch fails or times out."""
 import os
 import re
 import shutil
