@@ -599,7 +599,16 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
         elif emu:
             dpd = ctx.disp_per_dist_dev(te_raw.data_ptr(), te_f.data_ptr(),
                                         te_dist.data_ptr(), e_n, R, cond, C, D)
-            dpd[np.isnan(dpd)] = 0.05   # other ranks' rows (not run here)
+            # the other ranks' rows (not run here): interpolated over this
+            # rank's with a 2 % ripple, so the smoother sees a table of the
+            # usual shape (a piecewise-linear table drives the weighted
+            # lowess' rolling variance to ~0 and its fits degenerate)
+            for c in range(C):
+                fin = np.isfinite(dpd[:, c])
+                gap = ~fin & (np.arange(D) >= 4)
+                gi = np.flatnonzero(gap)
+                dpd[gap, c] = np.interp(gi, np.flatnonzero(fin), dpd[fin, c]) \
+                    * (1 + 0.02 * np.sin(1.7 * gi + c))
         else:
             dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                         t_dist.data_ptr(), n, R, cond, C, D)

@@ -201,16 +201,27 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
   ProfScope ps(ctx, "disp_nll", 0);
   auto k = k_brent<M>;
   constexpr int kBrentBlock = brent_block<M>();
+  const size_t lds_max = M <= 8 ? (size_t)ctx->brent_lds_kb * 1024 : 0;
   int& nb = ctx->resident[(const void*)k];
   if (nb == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBrentBlock, 0) != hipSuccess ||
+    if (lds_max)
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_max);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBrentBlock, lds_max) !=
+            hipSuccess ||
         nb < 1)
       nb = 1;
   }
   const int grid = std::max(1, std::min(S, ctx->n_cu * nb));
+  // LDS staging of each segment's head: the workgroup's whole share of the
+  // CU's LDS (one 1024-thread workgroup per CU), minus the static part
+  // (M >= 16: 512-thread workgroups, two per CU -- staging would halve that)
+  const size_t lds_bytes = M <= 8 ? (size_t)ctx->brent_lds_kb * 1024 : 0;
+  const int64_t lds_px = (int64_t)(lds_bytes / (8 * (size_t)M));
   (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), 0, ctx->stream, pd, n, seg_start, S,
-                     C, rep_idx, n_rep, st, seg_flags, result, queue, ctx->work_count);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), lds_px ? lds_px * 8 * M : 0,
+                     ctx->stream, pd, n, seg_start, S, C, rep_idx, n_rep, st, seg_flags,
+                     result, queue, ctx->work_count, lds_px);
 }
 
 // the gang variant (k_brent_gang): every live segment's search over the
@@ -378,6 +389,7 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_DISP_W2")) ctx->disp_w2 = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
   if (const char* e = std::getenv("H3D_BRENT")) ctx->brent_gang = std::atoi(e);
+  if (const char* e = std::getenv("H3D_BRENT_LDS_KB")) ctx->brent_lds_kb = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);

@@ -97,7 +97,10 @@ struct h3d_ctx {
   // H3D_BRENT: 1 = gang Brent searches (k_brent_gang) where one workgroup
   // per segment leaves CUs idle, 2 = always, 0 = k_brent only
   int brent_gang = 1;
-  int gang_aborts = 0;  // gang waits that timed out (fell back to k_brent)
+  int gang_aborts = 0;
+  // H3D_BRENT_LDS_KB: LDS per k_brent workgroup for the segment's staged
+  // head (0 = stream every evaluation from memory)
+  int brent_lds_kb = 144;  // gang waits that timed out (fell back to k_brent)
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
                     // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)
 };

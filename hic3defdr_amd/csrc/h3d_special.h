@@ -335,7 +335,8 @@ constexpr int kLogTabShifted = 53;  // buckets 0..53: m_i < sqrt(1/2)
 // Max error 1.3e-16 absolute, 4.2e-16 relative (80-bit reference over
 // [1e-300, 1e300] and [0.3, 3]) at about two thirds of the instructions of
 // the atanh-series form it replaces (one reciprocal, 11 series terms). Used
-// by the NLL sums only.
+// by the NLL sums (finite x > 0 by construction) and, through
+// log_fast_checked, the incomplete-gamma prefactor.
 H3D_HD double log_fast(double x) {
   int e;
   const double m = frexp(x, &e);  // [0.5, 1)
@@ -351,6 +352,17 @@ H3D_HD double log_fast(double x) {
   const double lp = fma(q, t * t, t);
   const double de = (double)(e - (i <= kLogTabShifted ? 1 : 0));
   return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + (tb.l + lp));
+}
+
+// log_fast for any x: frexp of 0 / inf would index outside the table, so x
+// is first replaced by 1 there and libm's values (-inf, inf, NaN) are
+// selected afterwards (the k_brent NLL keeps the unchecked form: the checks
+// cost it 8 %, r03 PMC)
+H3D_HD double log_fast_checked(double x) {
+  const bool ok = x > 0.0 && x < INFINITY;
+  const double v = log_fast(ok ? x : 1.0);
+  if (ok) return v;
+  return (x == INFINITY) ? INFINITY : (x == 0.0) ? -INFINITY : NAN;
 }
 
 // Stirling series of the NLL lgamma in r2 = 1/y^2 (8 Bernoulli terms),
@@ -538,13 +550,13 @@ H3D_HD double stirling_corr(double a) {
 // conditioning, a few ulp of |a ln x|, dominates their <= 1 ulp)
 H3D_HD double igam_fac_l(double a, double x, double lga) {
   if (fabs(a - x) > 0.4 * fabs(a) || a < 10.0) {
-    double ax = a * log_fast(x) - x - lga;
+    double ax = a * log_fast_checked(x) - x - lga;
     if (ax < -kMaxLog) return 0.0;
     return exp_fast(ax);
   }
   H3D_STAT(fac_l1, 1);
   double s = (x - a) / a;
-  return exp_fast(a * log1pmx(s) + 0.5 * log_fast(a / kTwoPi) - stirling_corr(a));
+  return exp_fast(a * log1pmx(s) + 0.5 * log_fast_checked(a / kTwoPi) - stirling_corr(a));
 }
 
 H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
@@ -1045,16 +1057,17 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
       igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
       if (fac == 0.0) return x;
       F = (upper ? Q : P) - t;
-      dP = div_fast(fac, x);
+      dP = fac / x;
       xe = x;
       Fe = F;
       dPe = dP;
     }
     // Newton ratio f / f' (f' = -P' on the upper tail), Halley correction
-    // (quotients to ~1 ulp: a Halley step's rounding does not reach the
-    // root it converges to)
-    const double f_fp = div_fast(upper ? -F : F, dP);
-    const double fpp_fp = -1.0 + div_fast(a - 1, x);
+    // f / f' and (a - 1) / x by IEEE divisions: P' and x reach the
+    // subnormal range deep in the tails (v_rcp_f64 flushes those); the
+    // Halley denominator ~1 takes the ~1-ulp quotient
+    const double f_fp = upper ? -F / dP : F / dP;
+    const double fpp_fp = -1.0 + (a - 1) / x;
     double xn = is_inf(fpp_fp) ? x - f_fp
                                : x - div_fast(f_fp, 1.0 - 0.5 * f_fp * fpp_fp);
     if (!(xn > 0.0)) xn = 0.5 * x;  // safeguard: stay in the support
