@@ -25,7 +25,7 @@ EXPORTS = [
     'h3d_version', 'h3d_device_count', 'h3d_open', 'h3d_close',
     'h3d_last_error', 'h3d_set_stream', 'h3d_union_count', 'h3d_union_fill',
     'h3d_size_factors_cmor', 'h3d_size_factors', 'h3d_disp_per_dist', 'h3d_disp_per_dist_dev',
-    'h3d_disp_table', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
+    'h3d_disp_table', 'h3d_disp_tables', 'h3d_lrt', 'h3d_lrt_dev', 'h3d_bh',
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
     'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
@@ -86,6 +86,7 @@ def load_library(path=None):
             'h3d_disp_per_dist_dev': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P,
                                            _I, _I, _P, _P, ALLREDUCE_FN, _P]),
             'h3d_disp_table': (_I, [_P, _I, _I, _D, _D, _P]),
+            'h3d_disp_tables': (_I, [_P, _I, _I, _I, _D, _D, _P]),
             'h3d_lrt': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I, _I, _P,
                              _P, _P, _P, _P]),
             'h3d_lrt_dev': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I, _I,
@@ -404,27 +405,18 @@ def disp_table(disp_per_dist_col, weighted=True, frac=None,
     return out
 
 
-_table_pool = None
-
-
 def disp_tables(disp_per_dist, weighted=True, frac=None, auto_frac_factor=15.):
     """disp_table for every column of ``disp_per_dist`` (D, C), the
-    conditions smoothed concurrently (ctypes drops the GIL inside libh3d, and
-    the smoother is a serial few-hundred-point computation per condition)."""
-    global _table_pool
-    d = np.asarray(disp_per_dist, dtype=np.float64)
-    C = d.shape[1]
-    def one(c):
-        return disp_table(d[:, c], weighted=weighted, frac=frac,
-                          auto_frac_factor=auto_frac_factor)
-    if C == 1:
-        return one(0)[:, None]
-    with _lock:
-        if _table_pool is None:
-            import concurrent.futures
-            _table_pool = concurrent.futures.ThreadPoolExecutor(
-                max_workers=8, thread_name_prefix='h3d_lowess')
-    return np.stack(list(_table_pool.map(one, range(C))), axis=1)
+    conditions smoothed on concurrent threads inside libh3d (one call)."""
+    lib = load_library()
+    d = _c(disp_per_dist, np.float64)
+    D, C = d.shape
+    out = np.empty((D, C))
+    _check(lib.h3d_disp_tables(_ptr(d), D, C, int(bool(weighted)),
+                               -1.0 if frac is None else float(frac),
+                               float(auto_frac_factor), _ptr(out)),
+           'h3d_disp_tables')
+    return out
 
 
 def bh(pvalues):

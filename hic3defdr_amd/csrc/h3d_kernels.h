@@ -294,11 +294,11 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           const bool on = k < nr;
           x[k] = on ? (double)raw_s[(int64_t)ri[k] * n + px] : 0.0;
           f[k] = on ? f_s[(int64_t)ri[k] * n + px] : 1.0;
-          lf[k] = on ? log(f[k]) : 0.0;
+          lf[k] = on ? log_fast_checked(f[k]) : 0.0;
           as[k] = alpha;
         }
         int fl = 0;
-        const double f_mean = exp(np_sum<MS>(lf, nr) / nr) - 0.0;
+        const double f_mean = exp_fast(np_sum<MS>(lf, nr) / nr) - 0.0;
         const double mu = fit_mu<MS>(x, f, as, nr, ~0u, &fl);
         if (fl) atomicOr(&seg_flags[s], fl);
         const double mu_out0 = mu * f_mean;

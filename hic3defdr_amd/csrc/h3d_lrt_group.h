@@ -89,10 +89,10 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
     *status |= kFlagNoRoot;
     return NAN;
   }
-  double th = log(init / cnt);
+  double th = log_fast_checked(init / cnt);
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
-    const double mu = exp(th);
+    const double mu = exp_fast(th);
     double g = 0.0, gp = 0.0;
 #pragma unroll
     for (int s = 0; s < J; ++s)
@@ -111,7 +111,7 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
     else
       return mu;
     const double dn = g / gp;
-    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp(th - dn);
+    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
     double tn = th - dn;
     if (!(tn > lo && tn < hi)) {
       if (is_inf(lo))
@@ -123,12 +123,12 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
     }
     const double step = fabs(tn - th);
     th = tn;
-    if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp(th);
+    if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp_fast(th);
     if (!is_inf(lo) && !is_inf(hi) && (hi - lo) <= 4e-16 * fmax(1.0, fabs(th)))
-      return exp(th);
+      return exp_fast(th);
   }
   *status |= kFlagNoConv;
-  return exp(th);
+  return exp_fast(th);
 }
 
 // M = 16 / 24 / 32 (R <= M), CM >= C. Same arguments and outputs as k_lrt.
@@ -229,11 +229,14 @@ __global__ __launch_bounds__(kBlock) void k_lrt8(
         if (c == cnd[s]) m1k = m1[c];
       const double xk = (double)x[s];
       const double r = 1.0 / a[s];
-      const double pre = lgam(r + xk) - lgam(xk + 1) - lgam(r) + r * log(r);
+      // the prefix is common to the null and alt rows and cancels in llr up
+      // to their rounding: the branch-light lgam_nll, as k_lrt
+      const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) +
+                         r * log_fast_checked(r);
       const double m0k = m0 * fv[s], m1f = m1k * fv[s];
-      const double l0 = log(r + m0k), l1 = log(r + m1f);
-      tn[s] = pre - r * l0 + xk * log(m0k) - xk * l0;
-      ta[s] = pre - r * l1 + xk * log(m1f) - xk * l1;
+      const double l0 = log_fast_checked(r + m0k), l1 = log_fast_checked(r + m1f);
+      tn[s] = pre - r * l0 + xk * log_fast_checked(m0k) - xk * l0;
+      ta[s] = pre - r * l1 + xk * log_fast_checked(m1f) - xk * l1;
     }
     const double lv = np_sum_g8<J>(tn, R, lane, base) - np_sum_g8<J>(ta, R, lane, base);
     fl_all |= st;

@@ -123,11 +123,13 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
     return NAN;
   }
   H3D_STAT(fit, 1);
-  double th = log(init / cnt);
+  // (the table log and straight-line exp of h3d_special.h: ~1 ulp, the
+  // OCML forms carried constant copies; the MLE is Newton-converged anyway)
+  double th = log_fast_checked(init / cnt);
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
     H3D_STAT(fit_it, 1);
-    const double mu = exp(th);
+    const double mu = exp_fast(th);
     double g = 0.0, gp = 0.0;
 #pragma unroll
     for (int k = 0; k < M; ++k)
@@ -150,7 +152,7 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
     // theta): once a step is <= 1e-8 the error after it is ~1e-16, so take
     // it and stop. (Without this exit, a final step below one ulp left th
     // on the bracket edge and fell through to ~50 bisections.)
-    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp(th - dn);
+    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
     double tn = th - dn;
     if (!(tn > lo && tn < hi)) {
       if (is_inf(lo))
@@ -162,12 +164,12 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
     }
     const double step = fabs(tn - th);
     th = tn;
-    if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp(th);
+    if (step <= 1e-15 * fmax(1.0, fabs(th))) return exp_fast(th);
     if (!is_inf(lo) && !is_inf(hi) && (hi - lo) <= 4e-16 * fmax(1.0, fabs(th)))
-      return exp(th);
+      return exp_fast(th);
   }
   *status |= kFlagNoConv;
-  return exp(th);
+  return exp_fast(th);
 }
 
 // ---- scipy.stats frozen-distribution methods as the reference calls them
@@ -330,11 +332,11 @@ H3D_HD int equalize_pixel(const double* x, const double* f, int n, double alpha,
   double lf[M], as[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    lf[k] = (k < n) ? log(f[k]) : 0.0;
+    lf[k] = (k < n) ? log_fast_checked(f[k]) : 0.0;
     as[k] = alpha;
   }
   // gmean(f, pseudocount=0, axis=1) = exp(nanmean(log f)) - 0
-  const double f_mean = exp(np_sum<M>(lf, n) / n) - 0.0;
+  const double f_mean = exp_fast(np_sum<M>(lf, n) / n) - 0.0;
   int st = 0;
   const double mu = fit_mu<M>(x, f, as, n, ~0u, &st);
   double mu_out = mu * f_mean;
@@ -411,11 +413,12 @@ H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
       // tests' 1e-10 absolute bar
       const double xk = (double)x[k];
       const double r = 1.0 / a[k];
-      const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) + r * log(r);
+      const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) +
+                         r * log_fast_checked(r);
       const double m0k = *mu0 * f[k], m1k = m1 * f[k];
-      const double l0 = log(r + m0k), l1 = log(r + m1k);
-      tn.add(k, pre - r * l0 + xk * log(m0k) - xk * l0);
-      ta.add(k, pre - r * l1 + xk * log(m1k) - xk * l1);
+      const double l0 = log_fast_checked(r + m0k), l1 = log_fast_checked(r + m1k);
+      tn.add(k, pre - r * l0 + xk * log_fast_checked(m0k) - xk * l0);
+      ta.add(k, pre - r * l1 + xk * log_fast_checked(m1k) - xk * l1);
     }
   }
   *llr = tn.sum() - ta.sum();

@@ -144,6 +144,12 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 int h3d_disp_table(const double* disp_per_dist_col, int D, int weighted,
                    double frac, double auto_frac_factor, double* table_out);
 
+/* h3d_disp_table for every column of disp_per_dist (D, C), row-major in and
+ * out, the conditions on concurrent host threads (analysis.py:208-219's
+ * per-condition loop). */
+int h3d_disp_tables(const double* disp_per_dist, int D, int C, int weighted,
+                    double frac, double auto_frac_factor, double* tables_out);
+
 /* ---- lrt --------------------------------------------------------------- */
 
 /* Per-pixel LRT (lrt.py:7-50) with disp[i, c] = disp_table[dist[i], c]

@@ -63,6 +63,25 @@ def test_disp_table_matches_e2e_disp_fn(lib, name):
 
 
 @pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3'])
+def test_disp_tables_all_conditions_in_one_call(lib, name):
+    """h3d_disp_tables (conditions on concurrent host threads) = one
+    h3d_disp_table per condition, bit for bit, and = the reference's disp_fn
+    tables; a degenerate column's error names its condition."""
+    g, kw = e2e_inputs(name)
+    dpd = g['disp_per_dist']
+    tabs = _native.disp_tables(dpd)
+    for c, cond in enumerate(kw['conds']):
+        np.testing.assert_array_equal(tabs[:, c],
+                                      _native.disp_table(dpd[:, c]))
+        assert rel_err(tabs[:, c], g['disp_fn_table__%s' % cond]) < 1e-12
+    bad = dpd.copy()
+    bad[:, -1] = np.nan
+    with pytest.raises(_native.H3DError, match='condition %d' % (
+            dpd.shape[1] - 1)):
+        _native.disp_tables(bad)
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9', 'r18c3'])
 def test_pickled_disp_fn_matches_reference_closure(lib, name):
     """DispFn (the product's picklable disp_fn) vs the reference's lowess
     closure evaluated at non-integer, negative and beyond-range distances."""
