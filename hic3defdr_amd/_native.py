@@ -33,6 +33,10 @@ EXPORTS = [
 ]
 
 
+# entry points a library built from an older tree may lack; callers check
+OPTIONAL = ('h3d_disp_tables',)
+
+
 class H3DError(RuntimeError):
     """A libh3d call failed (the reference would have raised too, or the
     native library / GPU is unavailable)."""
@@ -111,6 +115,8 @@ def load_library(path=None):
             'h3d_cml': (_I, [_P, _P, _I64, _I, _P]),
         }
         for name, (res, args) in sig.items():
+            if name in OPTIONAL and not hasattr(lib, name):
+                continue   # an older libh3d (A/B runs against past builds)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -411,6 +417,9 @@ def disp_tables(disp_per_dist, weighted=True, frac=None, auto_frac_factor=15.):
     lib = load_library()
     d = _c(disp_per_dist, np.float64)
     D, C = d.shape
+    if not hasattr(lib, 'h3d_disp_tables'):
+        return np.stack([disp_table(d[:, c], weighted, frac, auto_frac_factor)
+                         for c in range(C)], axis=1)
     out = np.empty((D, C))
     _check(lib.h3d_disp_tables(_ptr(d), D, C, int(bool(weighted)),
                                -1.0 if frac is None else float(frac),

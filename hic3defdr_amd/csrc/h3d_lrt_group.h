@@ -133,7 +133,10 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
 
 // M = 16 / 24 / 32 (R <= M), CM >= C. Same arguments and outputs as k_lrt.
 template <int M, int CM>
-__global__ __launch_bounds__(kBlock) void k_lrt8(
+// 2 waves per SIMD (<= 256 registers): with the table log in its logpmf
+// rows the M = 32 instantiation grew into AGPRs at 1 wave (cfg4 lrt 22.7 ->
+// 31.0 ms, r03i), so the rows keep OCML log here
+__global__ __launch_bounds__(kBlock, 2) void k_lrt8(
     const int32_t* __restrict__ raw, const double* __restrict__ f,
     const int32_t* __restrict__ dist, const double* __restrict__ table,
     int64_t n, int R, int C, int D, const int32_t* __restrict__ cond_of_rep,
@@ -232,11 +235,11 @@ __global__ __launch_bounds__(kBlock) void k_lrt8(
       // the prefix is common to the null and alt rows and cancels in llr up
       // to their rounding: the branch-light lgam_nll, as k_lrt
       const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) +
-                         r * log_fast_checked(r);
+                         r * log(r);
       const double m0k = m0 * fv[s], m1f = m1k * fv[s];
-      const double l0 = log_fast_checked(r + m0k), l1 = log_fast_checked(r + m1f);
-      tn[s] = pre - r * l0 + xk * log_fast_checked(m0k) - xk * l0;
-      ta[s] = pre - r * l1 + xk * log_fast_checked(m1f) - xk * l1;
+      const double l0 = log(r + m0k), l1 = log(r + m1f);
+      tn[s] = pre - r * l0 + xk * log(m0k) - xk * l0;
+      ta[s] = pre - r * l1 + xk * log(m1f) - xk * l1;
     }
     const double lv = np_sum_g8<J>(tn, R, lane, base) - np_sum_g8<J>(ta, R, lane, base);
     fl_all |= st;

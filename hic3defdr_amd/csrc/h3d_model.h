@@ -312,8 +312,17 @@ H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
     if (a_in >= 1.0 && a_out >= 1.0) {
       const double m_in = 1.0 - recip_fast(9.0 * a_in);
       const double m_out = 1.0 - recip_fast(9.0 * a_out);
+#if defined(__HIP_DEVICE_COMPILE__)
+      // single precision on gfx950 (v_log_f32 / v_exp_f32 / v_rsq_f32): the
+      // guess carries the approximation's own ~1e-4 error, 1e-7 more is
+      // nothing to Halley; the FP64 cbrt and sqrts were ~60 VALU
+      const float zz = (cbrtf((float)div_fast(xs, a_in)) - (float)m_in) *
+                       sqrtf((float)(9.0 * a_in));
+      const double y = m_out + (double)(zz * rsqrtf((float)(9.0 * a_out)));
+#else
       const double zz = (cbrt(div_fast(xs, a_in)) - m_in) * sqrt(9.0 * a_in);
       const double y = m_out + div_fast(zz, sqrt(9.0 * a_out));
+#endif
       if (y > 0.0) guess = a_out * y * y * y;
     }
     const double lga = (lga_out == lga_out) ? lga_out : lgam_cached(a_out, cache);

@@ -981,10 +981,13 @@ H3D_HD double find_inverse_gamma(double a, double p, double q, double lga) {
 // relative.
 constexpr int kTaylorK = 12;
 
+// (one ~1-ulp reciprocal of xe for both quotients: a window test, and a
+// subnormal xe -- 1/xe flushed to inf on gfx950 -- fails it safely)
 H3D_HD bool igam_taylor_ok(double a, double xe, double h) {
-  const double u = h / xe;
+  const double rx = recip_fast(xe);
+  const double u = h * rx;
   return xe > 0.0 && fabs(u) <= 0.05 &&
-         fabs(((a - 1.0) / xe - 1.0) * h) <= 0.4 &&
+         fabs(((a - 1.0) * rx - 1.0) * h) <= 0.4 &&
          fabs(a - 1.0) * u * u <= 0.25;
 }
 
@@ -1000,7 +1003,7 @@ H3D_HD void igam_step_taylor(double a, double xe, double h, double* dint,
                              double* ratio) {
   constexpr int K = kTaylorK;
   const double b = a - 1.0;
-  const double u = h / xe;
+  const double u = h * recip_fast(xe);  // xe normal: igam_taylor_ok held
   const double c0 = b - xe;
   double em1 = 0.0, e = 1.0;
   // integral_0^h = h sum E_k / (k+1); exp(g(h)) = sum E_k
