@@ -11,6 +11,9 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 300 \
   { tail -n 40 gpurun_out/${tag}_gpu_tests.log; exit 1; }
 timeout -k 10 120 python3 -u -c "import __graft_entry__ as g; g.smoke()" \
   > gpurun_out/${tag}_smoke.log 2>&1
+# the full-size cfg2 parity metrics (printed by the test)
+timeout -k 10 200 python3 -u -m pytest tests/test_gpu_scale.py -m gpu -rP -q --timeout 180 \
+  --timeout-method thread > gpurun_out/${tag}_scale_metrics.log 2>&1
 timeout -k 10 300 python3 -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
   -d gpurun_out/${tag}_prof -o run -- python3 -u bench.py --no-cpu-baseline --no-e2e \
