@@ -29,12 +29,12 @@ EXPORTS = [
     'h3d_profile_enable', 'h3d_profile_read', 'h3d_profile_reset',
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
     'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
-    'h3d_bh_ctx', 'h3d_bh_dev',
+    'h3d_bh_ctx', 'h3d_bh_dev', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
 ]
 
 
 # entry points a library built from an older tree may lack; callers check
-OPTIONAL = ('h3d_disp_tables',)
+OPTIONAL = ('h3d_disp_tables', 'h3d_npz_csr_info', 'h3d_npz_csr_read')
 
 
 class H3DError(RuntimeError):
@@ -113,6 +113,9 @@ def load_library(path=None):
             'h3d_lrt_wide': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I, _P,
                                   _P, _P, _P]),
             'h3d_cml': (_I, [_P, _P, _I64, _I, _P]),
+            'h3d_npz_csr_info': (_I, [ctypes.c_char_p, _P, _P, _P]),
+            'h3d_npz_csr_read': (_I, [ctypes.c_char_p, _I64, _I64, _P, _P, _P,
+                                      _P]),
         }
         for name, (res, args) in sig.items():
             if name in OPTIONAL and not hasattr(lib, name):
@@ -138,6 +141,47 @@ def _ptr(a):
 
 def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
+
+
+class CSR(object):
+    """The three arrays of a CSR matrix as the union kernels take them
+    (indptr int64, indices int32, data float64; the attribute names of
+    scipy.sparse.csr_matrix)."""
+
+    def __init__(self, indptr, indices, data, shape):
+        self.indptr, self.indices, self.data = indptr, indices, data
+        self.shape = shape
+
+
+def load_npz_csr(path):
+    """A scipy.sparse.save_npz CSR archive read by libh3d's zlib reader
+    (h3d_npz_csr_info / _read; the reference loads it with
+    scipy.sparse.load_npz, analysis.py:94,100). Rows whose columns are not
+    strictly increasing are canonicalised as scipy's sum_duplicates does.
+    Raises H3DError for archives the reader does not take (other sparse
+    formats, unsupported dtypes); the caller decides whether to use scipy."""
+    lib = load_library()
+    if not hasattr(lib, 'h3d_npz_csr_read'):
+        raise H3DError('libh3d.so predates h3d_npz_csr_read')
+    bp = os.fsencode(path)
+    n_rows, n_cols, nnz = _I64(0), _I64(0), _I64(0)
+    _check(lib.h3d_npz_csr_info(bp, ctypes.byref(n_rows), ctypes.byref(n_cols),
+                                ctypes.byref(nnz)), 'h3d_npz_csr_info')
+    indptr = np.empty(n_rows.value + 1, dtype=np.int64)
+    indices = np.empty(nnz.value, dtype=np.int32)
+    data = np.empty(nnz.value, dtype=np.float64)
+    canon = _I(0)
+    _check(lib.h3d_npz_csr_read(bp, n_rows.value, nnz.value, _ptr(indptr),
+                                _ptr(indices), _ptr(data), ctypes.byref(canon)),
+           'h3d_npz_csr_read')
+    shape = (n_rows.value, n_cols.value)
+    if canon.value:
+        return CSR(indptr, indices, data, shape)
+    import scipy.sparse as sparse
+    m = sparse.csr_matrix((data, indices, indptr), shape=shape)
+    m.sum_duplicates()
+    return CSR(_c(m.indptr, np.int64), _c(m.indices, np.int32),
+               _c(m.data, np.float64), shape)
 
 
 class Context(object):
@@ -169,7 +213,8 @@ class Context(object):
 
     # -- prepare_data -------------------------------------------------------
     def sparse_union(self, csrs, bias, dist_max):
-        """csrs: list of canonical scipy CSR (n_bins x n_bins); bias
+        """csrs: list of canonical CSR matrices (scipy or `CSR`, n_bins x
+        n_bins); bias
         (n_bins, R) filtered. Returns row, col (int32), raw (int64 (n, R)),
         balanced (float64 (n, R))."""
         R = len(csrs)

@@ -43,8 +43,16 @@ NATIVE_ESTIMATORS = ('qcml',)
 
 
 def _canonical_csr(fname):
+    """The replicate matrix as sorted, duplicate-free CSR rows (what the
+    union kernels expect): libh3d's zlib reader for the CSR archives
+    save_npz writes, scipy for any other sparse format load_npz takes
+    (analysis.py:94,100)."""
+    try:
+        return _native.load_npz_csr(fname)
+    except _native.H3DError:
+        pass   # scipy reads it (or raises as the reference would)
     m = sparse.load_npz(fname).tocsr()
-    m.sum_duplicates()  # sorted, duplicate-free rows (what the kernels expect)
+    m.sum_duplicates()
     return m
 
 

@@ -1,7 +1,8 @@
 """In-tree build of the native libraries (no cmake; plain hipcc / g++).
 
 - ``libh3d.so``          the product: C-ABI host code + gfx950 HIP kernels
-                          (csrc/h3d_api.hip, h3d_alt.hip, h3d_calls.cpp), loaded
+                          (csrc/h3d_api.hip, h3d_alt.hip, h3d_calls.cpp,
+                          h3d_npz.cpp; links zlib), loaded
                           by hic3defdr_amd._native.
 - ``libh3d_hosttest.so`` the device numerics compiled for the host, used only
                           by CPU unit tests (tests/test_special_host.py).
@@ -35,7 +36,7 @@ ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_lrt.hip', 'hipcc'),
                ('h3d_prepare_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
                ('h3d_bh.hip', 'hipcc'),
-               ('h3d_calls.cpp', 'g++')]
+               ('h3d_calls.cpp', 'g++'), ('h3d_npz.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
            'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h', 'h3d_lrt_group.h']
 # concurrent compiles (each hipcc TU is single-threaded; the box sets
@@ -119,7 +120,7 @@ def _link_native(force):
     out = os.path.join(LIBDIR, 'libh3d.so')
     objs = [o for o, _, _ in _native_objects()]
     cmd = [HIPCC, '--offload-arch=%s' % ARCH, '-shared', '-fPIC', '-o', out] \
-        + objs
+        + objs + ['-lz']
     return _build(out, cmd, objs, force)
 
 

@@ -425,6 +425,7 @@ void h3d_close(h3d_ctx* ctx) {
   if (ctx->work_count) (void)hipFree(ctx->work_count);
   if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_stage_done) (void)hipEventDestroy(ctx->h_stage_done);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -685,6 +686,10 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     q.off = blob;
     blob += (q.bytes + 255) & ~(size_t)255;
   }
+  if (!ctx->h_stage_done)
+    HIP_TRY(hipEventCreateWithFlags(&ctx->h_stage_done, hipEventDisableTiming));
+  else
+    HIP_TRY(hipEventSynchronize(ctx->h_stage_done));  // the previous copy has read it
   if (ctx->h_stage_bytes < blob) {
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     ctx->h_stage = nullptr;
@@ -697,6 +702,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   for (const Part& q : parts)
     if (q.bytes) std::memcpy((char*)ctx->h_stage + q.off, q.src, q.bytes);
   HIP_TRY(hipMemcpyAsync(d_blob, ctx->h_stage, blob, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(ctx->h_stage_done, s));
   int64_t* d_cs = (int64_t*)(d_blob + parts[0].off);
   int32_t* d_cl = (int32_t*)(d_blob + parts[1].off);
   int32_t* d_cd = (int32_t*)(d_blob + parts[2].off);

@@ -77,6 +77,10 @@ struct h3d_ctx {
   // pinned staging of estimate_disp's per-call tables (one H2D copy)
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
+  // recorded after each H2D copy out of h_stage: the next call waits on it
+  // before rewriting (or freeing) the buffer, whichever way the last call
+  // returned
+  hipEvent_t h_stage_done = nullptr;
   // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
   // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
   // 1 (distance, total count)

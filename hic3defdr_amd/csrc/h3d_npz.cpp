@@ -1,0 +1,427 @@
+// libh3d.so: native reader of the reference's contact-matrix input files --
+// scipy.sparse.save_npz archives (np.savez_compressed of indices / indptr /
+// data / format / shape; reference analysis.py:94,100 and
+// util/matrices.py:122-124 load them with scipy.sparse.load_npz). It replaces
+// the Python zipfile + numpy parse of prepare_data with: the zip central
+// directory read once, the three array members inflated by zlib on
+// concurrent threads straight into the caller's buffers in the dtypes the
+// union kernels take (indptr int64, indices int32, data float64), and the
+// canonical-CSR check (sorted, duplicate-free rows) done while converting.
+// Host code only (g++, -lz).
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "h3d.h"
+#include "h3d_errors.h"
+
+using h3derr::fail;
+
+namespace {
+
+uint16_t rd16(const unsigned char* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+uint32_t rd32(const unsigned char* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+         ((uint32_t)p[3] << 24);
+}
+uint64_t rd64(const unsigned char* p) {
+  return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32);
+}
+
+struct Member {
+  std::string name;
+  uint16_t method = 0;
+  uint32_t crc = 0;
+  uint64_t csize = 0, usize = 0, local_off = 0;
+};
+
+struct File {
+  FILE* f = nullptr;
+  ~File() {
+    if (f) fclose(f);
+  }
+};
+
+bool read_at(FILE* f, uint64_t off, void* buf, size_t n) {
+  if (fseeko(f, (off_t)off, SEEK_SET) != 0) return false;
+  return fread(buf, 1, n, f) == n;
+}
+
+// the zip central directory (EOCD, ZIP64 EOCD when present)
+int read_directory(FILE* f, std::vector<Member>* out) {
+  if (fseeko(f, 0, SEEK_END) != 0) return fail(H3D_EARG, "npz: seek failed");
+  const uint64_t size = (uint64_t)ftello(f);
+  const uint64_t tail = size < 65557 ? size : 65557;
+  std::vector<unsigned char> t(tail);
+  if (!read_at(f, size - tail, t.data(), tail)) return fail(H3D_EARG, "npz: read failed");
+  int64_t e = -1;
+  for (int64_t i = (int64_t)tail - 22; i >= 0; --i)
+    if (rd32(&t[i]) == 0x06054b50u) {
+      e = i;
+      break;
+    }
+  if (e < 0) return fail(H3D_EARG, "npz: no zip end record");
+  uint64_t n_ent = rd16(&t[e + 10]), cd_size = rd32(&t[e + 12]), cd_off = rd32(&t[e + 16]);
+  if ((n_ent == 0xFFFF || cd_off == 0xFFFFFFFFu) && e >= 20 &&
+      rd32(&t[e - 20]) == 0x07064b50u) {  // ZIP64 locator -> ZIP64 EOCD
+    unsigned char z[56];
+    if (!read_at(f, rd64(&t[e - 20 + 8]), z, 56) || rd32(z) != 0x06064b50u)
+      return fail(H3D_EARG, "npz: bad zip64 end record");
+    n_ent = rd64(z + 32);
+    cd_size = rd64(z + 40);
+    cd_off = rd64(z + 48);
+  }
+  std::vector<unsigned char> cd(cd_size);
+  if (!read_at(f, cd_off, cd.data(), cd_size)) return fail(H3D_EARG, "npz: read failed");
+  size_t p = 0;
+  for (uint64_t k = 0; k < n_ent; ++k) {
+    if (p + 46 > cd.size() || rd32(&cd[p]) != 0x02014b50u)
+      return fail(H3D_EARG, "npz: bad central directory");
+    Member m;
+    m.method = rd16(&cd[p + 10]);
+    m.crc = rd32(&cd[p + 16]);
+    m.csize = rd32(&cd[p + 20]);
+    m.usize = rd32(&cd[p + 24]);
+    const uint16_t nl = rd16(&cd[p + 28]), xl = rd16(&cd[p + 30]), cl = rd16(&cd[p + 32]);
+    m.local_off = rd32(&cd[p + 42]);
+    m.name.assign((const char*)&cd[p + 46], nl);
+    // ZIP64 extra field: the 0xFFFFFFFF fields follow in order
+    size_t x = p + 46 + nl;
+    const size_t xe = x + xl;
+    while (x + 4 <= xe) {
+      const uint16_t id = rd16(&cd[x]), len = rd16(&cd[x + 2]);
+      if (id == 0x0001) {
+        size_t q = x + 4;
+        if (m.usize == 0xFFFFFFFFu) m.usize = rd64(&cd[q]), q += 8;
+        if (m.csize == 0xFFFFFFFFu) m.csize = rd64(&cd[q]), q += 8;
+        if (m.local_off == 0xFFFFFFFFu) m.local_off = rd64(&cd[q]);
+      }
+      x += 4 + len;
+    }
+    out->push_back(m);
+    p += 46 + nl + xl + cl;
+  }
+  return 0;
+}
+
+// the zip CRC-32 of the member's bytes (zipfile raises BadZipFile on a
+// mismatch; so do we)
+// (zlib's table CRC runs ~0.5 GB/s: large members are split over threads
+// and the pieces joined with crc32_combine)
+uLong crc_range(const unsigned char* p, size_t n) {
+  uLong c = crc32(0L, Z_NULL, 0);
+  for (size_t o = 0; o < n; o += 1u << 30)
+    c = crc32(c, p + o, (uInt)std::min<size_t>(n - o, 1u << 30));
+  return c;
+}
+
+int check_crc(const Member& m, const std::vector<unsigned char>& b) {
+  const size_t kPiece = 4u << 20;
+  const int pieces = (int)std::min<size_t>(8, (b.size() + kPiece - 1) / kPiece);
+  uLong c;
+  if (pieces <= 1) {
+    c = crc_range(b.data(), b.size());
+  } else {
+    const size_t len = (b.size() + pieces - 1) / pieces;
+    std::vector<uLong> part(pieces);
+    std::vector<std::thread> th;
+    for (int i = 1; i < pieces; ++i)
+      th.emplace_back([&, i] {
+        const size_t o = i * len;
+        part[i] = crc_range(b.data() + o, std::min(len, b.size() - o));
+      });
+    part[0] = crc_range(b.data(), len);
+    for (auto& t : th) t.join();
+    c = part[0];
+    for (int i = 1; i < pieces; ++i)
+      c = crc32_combine(c, part[i], (z_off_t)std::min(len, b.size() - i * len));
+  }
+  if ((uint32_t)c != m.crc) return fail(H3D_EARG, "npz: CRC mismatch (%s)", m.name.c_str());
+  return 0;
+}
+
+// the member's bytes, inflated (method 8) or stored (0)
+int member_bytes(FILE* f, const Member& m, std::vector<unsigned char>* out) {
+  unsigned char lh[30];
+  if (!read_at(f, m.local_off, lh, 30) || rd32(lh) != 0x04034b50u)
+    return fail(H3D_EARG, "npz: bad local header (%s)", m.name.c_str());
+  const uint64_t data_off = m.local_off + 30 + rd16(lh + 26) + rd16(lh + 28);
+  std::vector<unsigned char> comp(m.csize);
+  if (m.csize && !read_at(f, data_off, comp.data(), m.csize))
+    return fail(H3D_EARG, "npz: read failed (%s)", m.name.c_str());
+  if (m.method == 0) {
+    out->swap(comp);
+    return check_crc(m, *out);
+  }
+  if (m.method != 8) return fail(H3D_EARG, "npz: compression method %d", (int)m.method);
+  out->resize(m.usize);
+  z_stream zs;
+  std::memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) return fail(H3D_EARG, "npz: inflateInit failed");
+  // the sizes may exceed uInt: feed and drain in chunks
+  uint64_t in_done = 0, out_done = 0;
+  int rc = Z_OK;
+  while (rc != Z_STREAM_END) {
+    if (zs.avail_in == 0 && in_done < m.csize) {
+      const uint64_t c = std::min<uint64_t>(m.csize - in_done, 1u << 30);
+      zs.next_in = comp.data() + in_done;
+      zs.avail_in = (uInt)c;
+      in_done += c;
+    }
+    if (zs.avail_out == 0) {
+      const uint64_t c = std::min<uint64_t>(m.usize - out_done, 1u << 30);
+      if (c == 0) break;
+      zs.next_out = out->data() + out_done;
+      zs.avail_out = (uInt)c;
+      out_done += c;
+    }
+    rc = inflate(&zs, Z_NO_FLUSH);
+    if (rc != Z_OK && rc != Z_STREAM_END) break;
+  }
+  inflateEnd(&zs);
+  if (rc != Z_STREAM_END || zs.total_out != m.usize)
+    return fail(H3D_EARG, "npz: inflate failed (%s)", m.name.c_str());
+  return check_crc(m, *out);
+}
+
+// the first `n` uncompressed bytes of the member (headers: no full inflate)
+int member_head(FILE* f, const Member& m, size_t n, std::vector<unsigned char>* out) {
+  unsigned char lh[30];
+  if (!read_at(f, m.local_off, lh, 30) || rd32(lh) != 0x04034b50u)
+    return fail(H3D_EARG, "npz: bad local header (%s)", m.name.c_str());
+  const uint64_t data_off = m.local_off + 30 + rd16(lh + 26) + rd16(lh + 28);
+  n = (size_t)std::min<uint64_t>(n, m.usize);
+  if (m.method == 0) {
+    out->resize(n);
+    if (n && !read_at(f, data_off, out->data(), n))
+      return fail(H3D_EARG, "npz: read failed (%s)", m.name.c_str());
+    return 0;
+  }
+  if (m.method != 8) return fail(H3D_EARG, "npz: compression method %d", (int)m.method);
+  const size_t cn = (size_t)std::min<uint64_t>(m.csize, n + 4096);
+  std::vector<unsigned char> comp(cn);
+  if (cn && !read_at(f, data_off, comp.data(), cn))
+    return fail(H3D_EARG, "npz: read failed (%s)", m.name.c_str());
+  out->resize(n);
+  z_stream zs;
+  std::memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, -MAX_WBITS) != Z_OK) return fail(H3D_EARG, "npz: inflateInit failed");
+  zs.next_in = comp.data();
+  zs.avail_in = (uInt)cn;
+  zs.next_out = out->data();
+  zs.avail_out = (uInt)n;
+  int rc = Z_OK;
+  while (zs.avail_out && rc == Z_OK) rc = inflate(&zs, Z_SYNC_FLUSH);
+  inflateEnd(&zs);
+  if (rc != Z_OK && rc != Z_STREAM_END && rc != Z_BUF_ERROR)
+    return fail(H3D_EARG, "npz: inflate failed (%s)", m.name.c_str());
+  out->resize(zs.total_out);
+  return 0;
+}
+
+// .npy header: dtype kind / size, C order, shape
+struct Npy {
+  char kind = 0;  // 'i', 'u', 'f', 'b', 'U', 'S'
+  int itemsize = 0;
+  bool little = true;
+  std::vector<int64_t> shape;
+  size_t data_off = 0;
+};
+
+int parse_npy(const std::vector<unsigned char>& b, Npy* h, const char* what) {
+  if (b.size() < 10 || std::memcmp(b.data(), "\x93NUMPY", 6) != 0)
+    return fail(H3D_EARG, "npz: %s is not a .npy", what);
+  const int major = b[6];
+  size_t hl, ho;
+  if (major == 1) {
+    hl = rd16(&b[8]);
+    ho = 10;
+  } else {
+    hl = rd32(&b[8]);
+    ho = 12;
+  }
+  if (ho + hl > b.size()) return fail(H3D_EARG, "npz: %s header truncated", what);
+  const std::string s((const char*)&b[ho], hl);
+  h->data_off = ho + hl;
+  const size_t d = s.find("'descr'");
+  const size_t q1 = s.find('\'', s.find(':', d) + 1);
+  const size_t q2 = s.find('\'', q1 + 1);
+  if (d == std::string::npos || q1 == std::string::npos || q2 == std::string::npos)
+    return fail(H3D_EARG, "npz: %s has no dtype", what);
+  const std::string descr = s.substr(q1 + 1, q2 - q1 - 1);  // e.g. <i4, |b1, <U3
+  if (descr.size() < 3) return fail(H3D_EARG, "npz: %s dtype %s", what, descr.c_str());
+  h->little = descr[0] != '>';
+  h->kind = descr[1];
+  h->itemsize = std::atoi(descr.c_str() + 2);
+  if (s.find("'fortran_order': True") != std::string::npos)
+    return fail(H3D_EARG, "npz: %s is Fortran-ordered", what);
+  const size_t sp = s.find('(', s.find("'shape'"));
+  const size_t se = s.find(')', sp);
+  size_t i = sp + 1;
+  while (i < se) {
+    while (i < se && (s[i] == ' ' || s[i] == ',')) ++i;
+    if (i >= se) break;
+    h->shape.push_back(std::atoll(s.c_str() + i));
+    while (i < se && s[i] != ',') ++i;
+  }
+  return 0;
+}
+
+int64_t npy_count(const Npy& h) {
+  int64_t n = 1;
+  for (int64_t v : h.shape) n *= v;
+  return n;
+}
+
+// element k of an integer / float .npy payload as T
+template <typename T>
+bool npy_convert(const std::vector<unsigned char>& b, const Npy& h, T* out, int64_t n) {
+  if (!h.little && h.itemsize > 1) return false;
+  if ((int64_t)(b.size() - h.data_off) < n * h.itemsize) return false;
+  const unsigned char* p = b.data() + h.data_off;
+#define H3D_CONV(CT)                               \
+  for (int64_t k = 0; k < n; ++k) {                \
+    CT v;                                          \
+    std::memcpy(&v, p + k * sizeof(CT), sizeof(CT)); \
+    out[k] = (T)v;                                 \
+  }                                                \
+  return true
+  if (h.kind == 'f' && h.itemsize == 8) { H3D_CONV(double); }
+  if (h.kind == 'f' && h.itemsize == 4) { H3D_CONV(float); }
+  if (h.kind == 'i' && h.itemsize == 8) { H3D_CONV(int64_t); }
+  if (h.kind == 'i' && h.itemsize == 4) { H3D_CONV(int32_t); }
+  if (h.kind == 'i' && h.itemsize == 2) { H3D_CONV(int16_t); }
+  if (h.kind == 'i' && h.itemsize == 1) { H3D_CONV(int8_t); }
+  if (h.kind == 'u' && h.itemsize == 8) { H3D_CONV(uint64_t); }
+  if (h.kind == 'u' && h.itemsize == 4) { H3D_CONV(uint32_t); }
+  if (h.kind == 'u' && h.itemsize == 2) { H3D_CONV(uint16_t); }
+  if ((h.kind == 'u' || h.kind == 'b') && h.itemsize == 1) { H3D_CONV(uint8_t); }
+#undef H3D_CONV
+  return false;
+}
+
+struct Archive {
+  File file;
+  std::vector<Member> members;
+  const Member* get(const char* name) const {
+    for (const Member& m : members)
+      if (m.name == name) return &m;
+    return nullptr;
+  }
+};
+
+int open_archive(const char* path, Archive* a) {
+  a->file.f = fopen(path, "rb");
+  if (!a->file.f) return fail(H3D_EARG, "npz: cannot open %s", path);
+  return read_directory(a->file.f, &a->members);
+}
+
+int small_member(Archive& a, const char* name, std::vector<unsigned char>* bytes, Npy* h) {
+  const Member* m = a.get(name);
+  if (!m) return fail(H3D_EARG, "npz: no %s member", name);
+  if (int rc = member_bytes(a.file.f, *m, bytes)) return rc;
+  return parse_npy(*bytes, h, name);
+}
+
+}  // namespace
+
+extern "C" {
+
+int h3d_npz_csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
+  if (!path || !n_rows || !n_cols || !nnz) return fail(H3D_EARG, "null argument");
+  Archive a;
+  if (int rc = open_archive(path, &a)) return rc;
+  std::vector<unsigned char> b;
+  Npy h;
+  if (int rc = small_member(a, "format.npy", &b, &h)) return rc;
+  const std::string fmt((const char*)b.data() + h.data_off, b.size() - h.data_off);
+  // format is a 0-d string array: 'csr' as UTF-32 ('<U3') or bytes ('|S3')
+  const bool csr = (h.kind == 'U' && b.size() >= h.data_off + 12 && b[h.data_off] == 'c' &&
+                    b[h.data_off + 4] == 's' && b[h.data_off + 8] == 'r') ||
+                   (h.kind == 'S' && fmt.compare(0, 3, "csr") == 0);
+  if (!csr) return fail(H3D_EARG, "npz: %s is not a CSR matrix", path);
+  if (int rc = small_member(a, "shape.npy", &b, &h)) return rc;
+  int64_t shp[2];
+  if (npy_count(h) != 2 || !npy_convert<int64_t>(b, h, shp, 2))
+    return fail(H3D_EARG, "npz: bad shape member");
+  const Member* md = a.get("data.npy");
+  if (!md) return fail(H3D_EARG, "npz: no data member");
+  // the data member's header: inflate its first bytes only
+  std::vector<unsigned char> head;
+  if (int rc = member_head(a.file.f, *md, 4096, &head)) return rc;
+  Npy hd;
+  if (int rc = parse_npy(head, &hd, "data.npy")) return rc;
+  *n_rows = shp[0];
+  *n_cols = shp[1];
+  *nnz = npy_count(hd);
+  return 0;
+}
+
+// the three arrays into caller buffers (n_rows + 1, nnz, nnz); *canonical =
+// 1 when every row's column indices are strictly increasing (sorted, no
+// duplicates: what the union kernels take as is)
+int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* indptr,
+                     int32_t* indices, double* data, int* canonical) {
+  if (!path || !indptr || (nnz && (!indices || !data)) || !canonical)
+    return fail(H3D_EARG, "null argument");
+  Archive a;
+  if (int rc = open_archive(path, &a)) return rc;
+  const char* names[3] = {"indptr.npy", "indices.npy", "data.npy"};
+  int rcs[3] = {0, 0, 0};
+  std::string errs[3];
+  auto work = [&](int j) {
+    const Member* m = a.get(names[j]);
+    if (!m) {
+      rcs[j] = fail(H3D_EARG, "npz: no %s member", names[j]);
+      errs[j] = h3derr::last();
+      return;
+    }
+    // each thread reads through its own FILE (one stream is not shareable)
+    File own;
+    own.f = fopen(path, "rb");
+    std::vector<unsigned char> b;
+    Npy h;
+    int rc = own.f ? member_bytes(own.f, *m, &b) : fail(H3D_EARG, "npz: reopen failed");
+    if (!rc) rc = parse_npy(b, &h, names[j]);
+    const int64_t want = j == 0 ? n_rows + 1 : nnz;
+    if (!rc && npy_count(h) != want)
+      rc = fail(H3D_EARG, "npz: %s has %lld entries, expected %lld", names[j],
+                (long long)npy_count(h), (long long)want);
+    bool ok = true;
+    if (!rc) {
+      if (j == 0) ok = npy_convert<int64_t>(b, h, indptr, want);
+      else if (j == 1) ok = npy_convert<int32_t>(b, h, indices, want);
+      else ok = npy_convert<double>(b, h, data, want);
+      if (!ok) rc = fail(H3D_EARG, "npz: %s dtype %c%d not supported", names[j], h.kind, h.itemsize);
+    }
+    rcs[j] = rc;
+    if (rc) errs[j] = h3derr::last();
+  };
+  std::thread t1(work, 1), t2(work, 2);
+  work(0);
+  t1.join();
+  t2.join();
+  for (int j = 0; j < 3; ++j)
+    if (rcs[j]) return fail(rcs[j], "%s", errs[j].c_str());
+  if (indptr[0] != 0 || indptr[n_rows] != nnz) return fail(H3D_EARG, "npz: bad indptr");
+  int canon = 1;
+  for (int64_t r = 0; r < n_rows && canon; ++r) {
+    if (indptr[r + 1] < indptr[r]) return fail(H3D_EARG, "npz: bad indptr");
+    for (int64_t k = indptr[r] + 1; k < indptr[r + 1]; ++k)
+      if (indices[k] <= indices[k - 1]) {
+        canon = 0;
+        break;
+      }
+  }
+  *canonical = canon;
+  return 0;
+}
+
+}  // extern "C"

@@ -89,6 +89,21 @@ int h3d_set_stream(h3d_ctx* ctx, void* stream);
 
 /* ---- prepare_data ------------------------------------------------------ */
 
+/* Native reader of the replicate contact matrices: scipy.sparse.save_npz
+ * archives as the reference loads them with scipy.sparse.load_npz
+ * (analysis/analysis.py:94,100 through util/matrices.py:122-124). Host only,
+ * no context. _info reads the archive's directory and the shape / format /
+ * data headers; _read inflates indptr, indices and data (zlib, one thread
+ * each) into caller buffers of n_rows + 1, nnz, nnz entries, converting to
+ * int64 / int32 / float64, and sets *canonical = 1 when every row's columns
+ * are strictly increasing (the layout h3d_union_count takes as is). H3D_EARG
+ * for a missing file, a non-CSR archive or an unsupported dtype. */
+int h3d_npz_csr_info(const char* path, int64_t* n_rows, int64_t* n_cols,
+                     int64_t* nnz);
+int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz,
+                     int64_t* indptr, int32_t* indices, double* data,
+                     int* canonical);
+
 /* Union pixel set of R upper-triangular CSR replicate matrices restricted to
  * 0 <= col-row <= dist_max and to bins whose bias is non-zero in every
  * replicate (matrices.py:92-129 with deconvolute(invert=True)). Two-pass:

@@ -1,0 +1,150 @@
+"""libh3d's native contact-matrix reader (h3d_npz_csr_info / _read,
+include/h3d.h) against scipy.sparse.load_npz, which the reference calls on
+the same files (analysis/analysis.py:94,100; util/matrices.py:122-124).
+Host code: runs without a GPU."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sparse
+
+from hic3defdr_amd import _native
+from hic3defdr_amd.analysis.analysis import _canonical_csr
+
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden', 'data')
+
+
+def _scipy_canonical(path):
+    m = sparse.load_npz(path).tocsr()
+    m.sum_duplicates()
+    return m
+
+
+def _same(ours, ref, native=True):
+    assert tuple(ours.shape) == tuple(ref.shape)
+    np.testing.assert_array_equal(ours.indptr, ref.indptr)
+    np.testing.assert_array_equal(ours.indices, ref.indices)
+    np.testing.assert_array_equal(ours.data, ref.data.astype(np.float64))
+    if not native:
+        return
+    assert ours.indptr.dtype == np.int64
+    assert ours.indices.dtype == np.int32
+    assert ours.data.dtype == np.float64
+
+
+def test_reads_every_golden_replicate_as_scipy():
+    files = sorted(glob.glob(os.path.join(GOLDEN, '*', '*', '*_raw.npz')))
+    assert len(files) >= 50
+    for p in files:
+        _same(_native.load_npz_csr(p), _scipy_canonical(p))
+
+
+@pytest.mark.parametrize('compressed', [True, False])
+@pytest.mark.parametrize('dtype', [np.int32, np.int64, np.float32,
+                                   np.float64, np.uint16])
+def test_dtypes_and_storage(tmp_path, compressed, dtype):
+    rng = np.random.default_rng(7)
+    n = 300
+    m = sparse.random(n, n, density=0.05, format='csr', random_state=3)
+    m = sparse.triu(m).tocsr()
+    m.data = rng.integers(1, 500, m.nnz).astype(dtype)
+    p = str(tmp_path / 'm.npz')
+    sparse.save_npz(p, m, compressed=compressed)
+    _same(_native.load_npz_csr(p), _scipy_canonical(p))
+
+
+def test_int64_index_arrays(tmp_path):
+    m = sparse.random(200, 200, density=0.1, format='csr', random_state=1)
+    m.indptr = m.indptr.astype(np.int64)
+    m.indices = m.indices.astype(np.int64)
+    p = str(tmp_path / 'm.npz')
+    sparse.save_npz(p, m)
+    assert np.load(p)['indices'].dtype == np.int64
+    _same(_native.load_npz_csr(p), _scipy_canonical(p))
+
+
+def test_unsorted_and_duplicate_columns_are_canonicalised(tmp_path):
+    # row 0: columns 5, 2, 5 (unsorted, duplicated); row 2: 1, 0
+    indptr = np.array([0, 3, 3, 5, 5], dtype=np.int32)
+    indices = np.array([5, 2, 5, 1, 0], dtype=np.int32)
+    data = np.array([1., 2., 3., 4., 5.])
+    m = sparse.csr_matrix((data, indices, indptr), shape=(4, 6))
+    assert not m.has_canonical_format
+    p = str(tmp_path / 'm.npz')
+    sparse.save_npz(p, m)
+    ours = _native.load_npz_csr(p)
+    _same(ours, _scipy_canonical(p))
+    np.testing.assert_array_equal(ours.indices, [2, 5, 0, 1])
+    np.testing.assert_array_equal(ours.data, [2., 4., 5., 4.])
+
+
+def test_empty_matrix(tmp_path):
+    m = sparse.csr_matrix((50, 50))
+    p = str(tmp_path / 'm.npz')
+    sparse.save_npz(p, m)
+    ours = _native.load_npz_csr(p)
+    _same(ours, _scipy_canonical(p))
+    assert ours.indices.size == 0 and ours.indptr.size == 51
+
+
+def test_non_csr_archive_goes_through_scipy(tmp_path):
+    m = sparse.random(40, 40, density=0.2, format='coo', random_state=0)
+    p = str(tmp_path / 'm.npz')
+    sparse.save_npz(p, m)
+    with pytest.raises(_native.H3DError, match='not a CSR'):
+        _native.load_npz_csr(p)
+    got = _canonical_csr(p)        # the prepare_data loader falls back
+    _same(got, _scipy_canonical(p), native=False)
+
+
+def test_missing_and_corrupt_files(tmp_path):
+    with pytest.raises(_native.H3DError):
+        _native.load_npz_csr(str(tmp_path / 'nope.npz'))
+    with pytest.raises(FileNotFoundError):
+        _canonical_csr(str(tmp_path / 'nope.npz'))   # as load_npz raises
+    bad = tmp_path / 'bad.npz'
+    bad.write_bytes(b'not a zip archive at all' * 10)
+    with pytest.raises(_native.H3DError):
+        _native.load_npz_csr(str(bad))
+    # truncated archive: the directory is gone
+    m = sparse.random(100, 100, density=0.1, format='csr', random_state=0)
+    good = str(tmp_path / 'good.npz')
+    sparse.save_npz(good, m)
+    raw = open(good, 'rb').read()
+    trunc = tmp_path / 'trunc.npz'
+    trunc.write_bytes(raw[:len(raw) // 2])
+    with pytest.raises(_native.H3DError):
+        _native.load_npz_csr(str(trunc))
+    # one flipped byte inside a stored member's payload: the zip CRC-32
+    plain = str(tmp_path / 'plain.npz')
+    sparse.save_npz(plain, m, compressed=False)
+    raw = bytearray(open(plain, 'rb').read())
+    k = raw.find(b'data.npy') + 8 + 200   # local header name, then payload
+    raw[k] ^= 0xFF
+    flipped = tmp_path / 'flipped.npz'
+    flipped.write_bytes(bytes(raw))
+    with pytest.raises(_native.H3DError, match='CRC'):
+        _native.load_npz_csr(str(flipped))
+
+
+def test_large_member_zip64(tmp_path):
+    # ~40 MB data member, written with zipfile's ZIP64 extensions forced
+    import zipfile
+    n, nnz = 1000, 5_000_000
+    rng = np.random.default_rng(0)
+    counts = np.full(n, nnz // n)
+    indptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    # strictly increasing columns in every row
+    indices = np.tile(np.arange(nnz // n, dtype=np.int32) * 3, n)
+    data = rng.integers(1, 100, nnz).astype(np.float64)
+    p = str(tmp_path / 'z.npz')
+    with zipfile.ZipFile(p, 'w', compression=zipfile.ZIP_DEFLATED,
+                         allowZip64=True) as z:
+        for name, arr in [('indices', indices), ('indptr', indptr),
+                          ('format', np.array('csr')),
+                          ('shape', np.array([n, 100000])), ('data', data)]:
+            with z.open(name + '.npy', 'w', force_zip64=True) as fh:
+                np.lib.format.write_array(fh, np.asanyarray(arr))
+    ref = _scipy_canonical(p)
+    _same(_native.load_npz_csr(p), ref)
