@@ -5,8 +5,9 @@ Workloads (BASELINE.json configs):
   bins, 4 replicates (2 + 2 conditions), dist_thresh_max 250 (SURVEY.md §8(d)
   generator, seed = rank). Untimed setup: generate the input files, run the
   product's GPU prepare_data, upload raw / f / dist of the disp pixels to
-  HBM. One step = estimate_disp (qcml per distance x condition, lowess
-  smoothing table) + lrt (fused per-pixel GLM fits + LRT) on the resident
+  HBM. One step = estimate_disp (qcml per distance x condition) + the lowess
+  smoothing tables (on the GPU, h3d_disp_tables_dev; H3D_DEV_TABLE=0 for the
+  host smoother) + lrt (fused per-pixel GLM fits + LRT) on the resident
   inputs, outputs left in HBM.
 - cfg3 (configs[2], the N > 1 default; --config cfg3 at any N): the whole
   mouse genome at 10 kb -- 20 mm10-sized chromosomes, 4 replicates, dmax 200,
@@ -333,6 +334,35 @@ def _upload(torch, dev, raw, f, dist_np):
             torch.from_numpy(np.ascontiguousarray(dist_np, dtype=np.int32)).to(dev))
 
 
+def table_lrt(torch, dev, ctx, D, C):
+    """The step's dispersion table -> LRT: on the device (h3d_disp_tables_dev
+    then h3d_lrt_dev_tab: the per-distance estimates go up once, the smoother
+    runs on the GPU, nothing waits in between) unless H3D_DEV_TABLE=0, which
+    keeps the host smoother (h3d_disp_tables) and uploads its table."""
+    from hic3defdr_amd import _native
+    use_dev = os.environ.get('H3D_DEV_TABLE', '1') != '0' and \
+        hasattr(ctx.lib, 'h3d_disp_tables_dev')
+    pin = torch.empty((D, C), dtype=torch.float64).pin_memory()
+    t_dpd = torch.empty((D, C), dtype=torch.float64, device=dev)
+    t_tab = torch.empty_like(t_dpd)
+
+    def run(dpd, t_raw, t_f, t_dist, n, R, cond, o):
+        ptrs = (o['p'].data_ptr(), o['llr'].data_ptr(), o['mu0'].data_ptr(),
+                o['mu1'].data_ptr(), o['disp'].data_ptr())
+        if use_dev:
+            pin.numpy()[...] = dpd
+            t_dpd.copy_(pin, non_blocking=True)   # the ctx's stream
+            ctx.disp_tables_dev(t_dpd.data_ptr(), D, C, t_tab.data_ptr())
+            ctx.lrt_dev_tab(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
+                            t_tab.data_ptr(), D, n, R, cond, *ptrs)
+        else:
+            tab = _native.disp_tables(dpd)
+            ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
+                        tab, n, R, cond, *ptrs)
+    run.on_device = use_dev
+    return run
+
+
 def timed_run(args, ctx, dist, dev, step):
     """W untimed steps, then exactly K timed steps between barrier +
     synchronize on both sides (HIP events on the roofline kernels inside),
@@ -496,6 +526,8 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
             def reduce(ptr, count):
                 pass
 
+        tl = table_lrt(torch, dev, ctx, D, C)
+
         def step():
             if by_dist:
                 dpd = parallel.disp_per_dist_by_distance(
@@ -504,11 +536,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
                 dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                             t_dist.data_ptr(), n, R, cond, C,
                                             D, reduce=reduce)
-            tab = _native.disp_tables(dpd)
-            ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
-                        tab, n, R, cond, o['p'].data_ptr(), o['llr'].data_ptr(),
-                        o['mu0'].data_ptr(), o['mu1'].data_ptr(),
-                        o['disp'].data_ptr())
+            tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
             return dpd
 
         elapsed, ev, per = timed_run(args, ctx, dist, dev, step)
@@ -592,6 +620,8 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
         ctx.bh_dev(t.data_ptr(), t.numel(), q.data_ptr())
         return q
 
+    tl = table_lrt(torch, dev, ctx, D, C)
+
     def step():
         if world > 1:
             dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
@@ -612,11 +642,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
         else:
             dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                         t_dist.data_ptr(), n, R, cond, C, D)
-        tab = _native.disp_tables(dpd)
-        ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(), tab,
-                    n, R, cond, o['p'].data_ptr(), o['llr'].data_ptr(),
-                    o['mu0'].data_ptr(), o['mu1'].data_ptr(),
-                    o['disp'].data_ptr())
+        tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
         if world > 1:
             o['q'] = parallel.bh_all_ranks(o['p'], bh_fn)
         else:

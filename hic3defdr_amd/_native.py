@@ -30,11 +30,13 @@ EXPORTS = [
     'h3d_find_clusters', 'h3d_format_clusters', 'h3d_lrt_poisson',
     'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
     'h3d_bh_ctx', 'h3d_bh_dev', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
+    'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
 ]
 
 
 # entry points a library built from an older tree may lack; callers check
-OPTIONAL = ('h3d_disp_tables', 'h3d_npz_csr_info', 'h3d_npz_csr_read')
+OPTIONAL = ('h3d_disp_tables', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
+            'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab')
 
 
 class H3DError(RuntimeError):
@@ -113,6 +115,10 @@ def load_library(path=None):
             'h3d_lrt_wide': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I, _P,
                                   _P, _P, _P]),
             'h3d_cml': (_I, [_P, _P, _I64, _I, _P]),
+            'h3d_disp_tables_dev': (_I, [_P, _P, _I, _I, _I, _D, _D, _P]),
+            'h3d_disp_tables_wait': (_I, [_P]),
+            'h3d_lrt_dev_tab': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I,
+                                     _I, _P, _P, _P, _P, _P]),
             'h3d_npz_csr_info': (_I, [ctypes.c_char_p, _P, _P, _P]),
             'h3d_npz_csr_read': (_I, [ctypes.c_char_p, _I64, _I64, _P, _P, _P,
                                       _P]),
@@ -383,6 +389,29 @@ class Context(object):
             self.handle, d_raw, d_f, d_dist, _ptr(tab), n, R, C, _ptr(cond),
             D, int(bool(refit_mu)), d_p, d_llr, d_mu0, d_mu1, d_disp),
             'h3d_lrt_dev')
+
+    def disp_tables_dev(self, d_dpd, D, C, d_tables, weighted=True,
+                        frac=None, auto_frac_factor=15.):
+        """disp_tables on the GPU: device (D, C) float64 in and out, enqueued
+        without waiting (settled by lrt_dev_tab or disp_tables_wait)."""
+        _check(self.lib.h3d_disp_tables_dev(
+            self.handle, d_dpd, D, C, int(bool(weighted)),
+            -1.0 if frac is None else float(frac), float(auto_frac_factor),
+            d_tables), 'h3d_disp_tables_dev')
+
+    def disp_tables_wait(self):
+        _check(self.lib.h3d_disp_tables_wait(self.handle),
+               'h3d_disp_tables_wait')
+
+    def lrt_dev_tab(self, d_raw, d_f, d_dist, d_table, D, n, R, cond_of_rep,
+                    d_p, d_llr, d_mu0, d_mu1, d_disp=None, refit_mu=True):
+        """lrt_dev with the (D, C) table in device memory."""
+        cond = _c(cond_of_rep, np.int32)
+        C = int(cond.max()) + 1
+        _check(self.lib.h3d_lrt_dev_tab(
+            self.handle, d_raw, d_f, d_dist, d_table, n, R, C, _ptr(cond),
+            D, int(bool(refit_mu)), d_p, d_llr, d_mu0, d_mu1, d_disp),
+            'h3d_lrt_dev_tab')
 
     # -- alternative models (analysis/alternatives.py) -----------------------
     def lrt_poisson(self, raw, f, cond_of_rep, C):

@@ -35,7 +35,7 @@ ARCH = os.environ.get('H3D_OFFLOAD_ARCH', 'gfx950')
 # (source, compiler): device TUs through hipcc, host-only TUs through g++
 NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_lrt.hip', 'hipcc'),
                ('h3d_prepare_api.hip', 'hipcc'), ('h3d_alt.hip', 'hipcc'),
-               ('h3d_bh.hip', 'hipcc'),
+               ('h3d_bh.hip', 'hipcc'), ('h3d_table.hip', 'hipcc'),
                ('h3d_calls.cpp', 'g++'), ('h3d_npz.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
            'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h', 'h3d_lrt_group.h']

@@ -49,6 +49,16 @@ struct ProfEntry {
   int64_t units = 0;
 };
 
+// a device dispersion table enqueued by h3d_disp_tables_dev whose status
+// has not been read yet (h3d_lrt_dev_tab / h3d_disp_tables_wait settle it)
+struct TablePending {
+  const double* dpd = nullptr;
+  double* tables = nullptr;
+  int D = 0, C = 0, weighted = 1;
+  double frac = -1.0, aff = 15.0;
+  int active = 0, on_host = 0;
+};
+
 }  // namespace h3dint
 
 struct h3d_ctx {
@@ -105,6 +115,7 @@ struct h3d_ctx {
   // H3D_BRENT_LDS_KB: LDS per k_brent workgroup for the segment's staged
   // head (0 = stream every evaluation from memory)
   int brent_lds_kb = 144;  // gang waits that timed out (fell back to k_brent)
+  h3dint::TablePending tab_pending;
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
                     // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)
 };
@@ -129,6 +140,10 @@ int check_cond(const int32_t* cond_of_rep, int R, int C, std::vector<int>* nrep,
                std::vector<int32_t>* rep_idx);
 // kernel status flags -> H3D_E* code (+ message)
 int flags_to_code(int fl);
+// the device table of h3d_disp_tables_dev (h3d_table.hip): copy its status
+// (before the stream sync), settle it (after): 1 = redone on the host
+int table_status_copy(h3d_ctx* ctx, int* h_st);
+int table_settle(h3d_ctx* ctx, const int* h_st);
 
 // wraps one kernel launch with HIP events on the ctx stream when profiling
 struct ProfScope {

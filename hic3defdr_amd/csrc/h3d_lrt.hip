@@ -37,11 +37,12 @@ void launch_lrt(h3d_ctx* ctx, const int32_t* raw, const double* f,
 }
 
 // wide: disp_table is per pixel AND replicate (n, R) (d_dist must be null)
+// table_on_dev: disp_table is a device buffer (h3d_disp_tables_dev's output)
 int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
             const int32_t* d_dist, const double* disp_table, int64_t n, int R,
             int C, const int32_t* cond_of_rep, int D, int refit_mu, double* d_p,
             double* d_llr, double* d_mu0, double* d_mu1, double* d_disp,
-            int wide) {
+            int wide, int table_on_dev = 0) {
   if (!ctx || !disp_table || !cond_of_rep) return fail(H3D_EARG, "null argument");
   if (wide && (d_dist || d_disp)) return fail(H3D_EARG, "wide dispersions take no dist / disp_out");
   if (n == 0) return 0;
@@ -55,11 +56,13 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   // d_dist == NULL: disp_table holds per-pixel dispersions (n, C), or with
   // `wide` per pixel and replicate (n, R)
   const size_t tab_n = d_dist ? (size_t)D * C : (size_t)n * (wide ? R : C);
-  double* d_tab = (double*)scratch(ctx, "disp_table", tab_n * 8);
+  double* d_tab = table_on_dev ? (double*)disp_table
+                               : (double*)scratch(ctx, "disp_table", tab_n * 8);
   int32_t* d_cond = (int32_t*)scratch(ctx, "cond_of_rep", R * 4);
   int* d_fl = (int*)scratch(ctx, "lrt_flags", 4);
   if (!d_tab || !d_cond || !d_fl) return fail(H3D_ENOMEM, "lrt scratch");
-  HIP_TRY(hipMemcpyAsync(d_tab, disp_table, tab_n * 8, hipMemcpyHostToDevice, s));
+  if (!table_on_dev)
+    HIP_TRY(hipMemcpyAsync(d_tab, disp_table, tab_n * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d_cond, cond_of_rep, R * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
   {
@@ -83,8 +86,19 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   HIP_TRY(hipGetLastError());
   int fl = 0;
+  int tst[kMaxConds];
+  const int tab_check = table_on_dev ? table_status_copy(ctx, tst) : 0;
+  if (tab_check < 0) return tab_check;
   HIP_TRY(hipMemcpyAsync(&fl, d_fl, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (tab_check) {
+    // a device table the host had to redo: the LRT over it again
+    const int ts = table_settle(ctx, tst);
+    if (ts < 0) return ts;
+    if (ts == 1)
+      return lrt_run(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep, D,
+                     refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, wide, 1);
+  }
   return flags_to_code(fl);
 }
 
@@ -139,6 +153,16 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                 double* d_disp) {
   return lrt_run(ctx, d_raw, d_f, d_dist, disp_table, n, R, C, cond_of_rep, D, refit_mu,
                  d_p, d_llr, d_mu0, d_mu1, d_disp, 0);
+}
+
+int h3d_lrt_dev_tab(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                    const int32_t* d_dist, const double* d_disp_table, int64_t n,
+                    int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
+                    double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
+                    double* d_disp) {
+  if (!d_dist) return fail(H3D_EARG, "h3d_lrt_dev_tab takes a per-distance table");
+  return lrt_run(ctx, d_raw, d_f, d_dist, d_disp_table, n, R, C, cond_of_rep, D,
+                 refit_mu, d_p, d_llr, d_mu0, d_mu1, d_disp, 0, 1);
 }
 
 int h3d_lrt_wide(h3d_ctx* ctx, const int64_t* raw, const double* f,

@@ -165,6 +165,19 @@ int h3d_disp_table(const double* disp_per_dist_col, int D, int weighted,
 int h3d_disp_tables(const double* disp_per_dist, int D, int C, int weighted,
                     double frac, double auto_frac_factor, double* tables_out);
 
+/* The same tables computed on the GPU (one workgroup per condition, D <=
+ * 1024; larger D runs the host smoother inside the call), device buffers
+ * in and out, enqueued on the ctx stream without waiting: the estimate_disp
+ * -> lrt step stays on the device (analysis.py:226-240 between :198-246 and
+ * :249-276). Its status is settled by the next h3d_lrt_dev_tab (which
+ * re-runs the LRT if a degenerate fit had to be redone on the host) or by
+ * h3d_disp_tables_wait; both return the reference's error as
+ * h3d_disp_tables would. The buffers must stay valid until then. */
+int h3d_disp_tables_dev(h3d_ctx* ctx, const double* d_disp_per_dist, int D,
+                        int C, int weighted, double frac,
+                        double auto_frac_factor, double* d_tables_out);
+int h3d_disp_tables_wait(h3d_ctx* ctx);
+
 /* ---- lrt --------------------------------------------------------------- */
 
 /* Per-pixel LRT (lrt.py:7-50) with disp[i, c] = disp_table[dist[i], c]
@@ -182,6 +195,14 @@ int h3d_lrt_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                 int R, int C, const int32_t* cond_of_rep, int D, int refit_mu,
                 double* d_p, double* d_llr, double* d_mu0, double* d_mu1,
                 double* d_disp);
+
+/* h3d_lrt_dev with the per-distance table (D, C) in DEVICE memory (from
+ * h3d_disp_tables_dev; d_dist required). */
+int h3d_lrt_dev_tab(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                    const int32_t* d_dist, const double* d_disp_table,
+                    int64_t n, int R, int C, const int32_t* cond_of_rep, int D,
+                    int refit_mu, double* d_p, double* d_llr, double* d_mu0,
+                    double* d_mu1, double* d_disp);
 
 /* lrt.py:7-50 with the reference's own disp argument: per pixel AND
  * replicate dispersions disp_wide (n, R) (lrt.py's `disp`, as analysis.py:277
