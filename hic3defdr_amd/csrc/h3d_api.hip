@@ -404,6 +404,7 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
   if (const char* e = std::getenv("H3D_BRENT")) ctx->brent_gang = std::atoi(e);
   if (const char* e = std::getenv("H3D_BRENT_LDS_KB")) ctx->brent_lds_kb = std::atoi(e);
+  if (const char* e = std::getenv("H3D_DEV_SEG_TABLES")) ctx->dev_seg_tables = std::atoi(e);
   if (hipMalloc((void**)&ctx->work_count, 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(ctx->work_count, 0, 2 * sizeof(unsigned long long)) != hipSuccess) {
     (void)hipStreamDestroy(ctx->own);
@@ -491,6 +492,12 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   const int S = D * C;
   const int maxnr = *std::max_element(nrep.begin(), nrep.end());
   HostStamps stamp;
+  // the per-call tables built on the device (k_disp_tables), no host sync
+  // before the qcml loop -- single rank, and enough segments that the Brent
+  // searches need no gangs (whose task tables the host builds from the
+  // segment bounds)
+  const bool dev_tables = ctx->dev_seg_tables && !reduce && n > 0 &&
+                          ctx->brent_gang != 2 && (S >= ctx->n_cu || ctx->brent_gang == 0);
 
   // 1. stable sort of the pixels by distance, SoA gather
   std::vector<int64_t> seg_start(D + 1, 0);
@@ -622,14 +629,18 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     }
     hipLaunchKernelGGL(k_seg_bounds, dim3((D + 1 + 255) / 256), dim3(256), 0, s,
                        dist_s, n, D, d_seg);
-    HIP_TRY(hipMemcpyAsync(seg_start.data(), d_seg, (D + 1) * 8,
-                           hipMemcpyDeviceToHost, s));
-    stamp("prep launched");
-    HIP_TRY(hipStreamSynchronize(s));
-    if (seg_start[0] != 0 || seg_start[D] != n) {
-      stamp("seg_start synced (dist check failed)");
-      // pixels with dist < 0 or >= D
-      return fail(H3D_EARG, "dist outside [0, %d)", D);
+    if (!dev_tables) {
+      HIP_TRY(hipMemcpyAsync(seg_start.data(), d_seg, (D + 1) * 8,
+                             hipMemcpyDeviceToHost, s));
+      stamp("prep launched");
+      HIP_TRY(hipStreamSynchronize(s));
+      if (seg_start[0] != 0 || seg_start[D] != n) {
+        stamp("seg_start synced (dist check failed)");
+        // pixels with dist < 0 or >= D
+        return fail(H3D_EARG, "dist outside [0, %d)", D);
+      }
+    } else {
+      stamp("prep launched");
     }
   }
 
@@ -637,35 +648,39 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   stamp("seg_start synced");
   std::vector<int64_t> cs;
   std::vector<int32_t> cl, cd, scb(D), sce(D);
-  for (int d = 0; d < D; ++d) {
-    scb[d] = (int32_t)cl.size();
-    for (int64_t a = seg_start[d]; a < seg_start[d + 1]; a += kChunk) {
-      cs.push_back(a);
-      cl.push_back((int32_t)std::min<int64_t>(kChunk, seg_start[d + 1] - a));
-      cd.push_back(d);
-    }
-    sce[d] = (int32_t)cl.size();
-  }
-  const int n_chunks = (int)cl.size();
-
-  // global pixel counts per segment (all ranks)
-  std::vector<double> cnt(S, 0.0);
-  for (int d = 0; d < D; ++d)
-    for (int c = 0; c < C; ++c) cnt[d * C + c] = (double)(seg_start[d + 1] - seg_start[d]);
-  double* d_cnt = (double*)scratch(ctx, "seg_cnt", S * 8);
-  if (!d_cnt) return fail(H3D_ENOMEM, "seg_cnt");
-  if (reduce) {
-    HIP_TRY(hipMemcpyAsync(d_cnt, cnt.data(), S * 8, hipMemcpyHostToDevice, s));
-    if (reduce(d_cnt, S, user)) return fail(H3D_EHIP, "allreduce callback failed");
-    HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, S * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-  }
-
   std::vector<SegState> st(S);
-  for (int sg = 0; sg < S; ++sg) seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C]);
   std::vector<int64_t> lpx(S);
-  for (int d = 0; d < D; ++d)
-    for (int c = 0; c < C; ++c) lpx[d * C + c] = seg_start[d + 1] - seg_start[d];
+  int n_chunks = 0;
+  if (dev_tables) {
+    n_chunks = (int)std::min<int64_t>(n / kChunk + D + 1, INT32_MAX);  // an upper bound
+  } else {
+    for (int d = 0; d < D; ++d) {
+      scb[d] = (int32_t)cl.size();
+      for (int64_t a = seg_start[d]; a < seg_start[d + 1]; a += kChunk) {
+        cs.push_back(a);
+        cl.push_back((int32_t)std::min<int64_t>(kChunk, seg_start[d + 1] - a));
+        cd.push_back(d);
+      }
+      sce[d] = (int32_t)cl.size();
+    }
+    n_chunks = (int)cl.size();
+
+    // global pixel counts per segment (all ranks)
+    std::vector<double> cnt(S, 0.0);
+    for (int d = 0; d < D; ++d)
+      for (int c = 0; c < C; ++c) cnt[d * C + c] = (double)(seg_start[d + 1] - seg_start[d]);
+    double* d_cnt = (double*)scratch(ctx, "seg_cnt", S * 8);
+    if (!d_cnt) return fail(H3D_ENOMEM, "seg_cnt");
+    if (reduce) {
+      HIP_TRY(hipMemcpyAsync(d_cnt, cnt.data(), S * 8, hipMemcpyHostToDevice, s));
+      if (reduce(d_cnt, S, user)) return fail(H3D_EHIP, "allreduce callback failed");
+      HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, S * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    for (int sg = 0; sg < S; ++sg) seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C]);
+    for (int d = 0; d < D; ++d)
+      for (int c = 0; c < C; ++c) lpx[d * C + c] = seg_start[d + 1] - seg_start[d];
+  }
 
   // the per-call tables go up as ONE copy from a pinned staging buffer (nine
   // pageable copies cost ~0.3 ms of host-side gaps per cfg2 step: each
@@ -675,9 +690,12 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     const void* src;
     size_t bytes, off;
   };
-  Part parts[] = {{cs.data(), cs.size() * 8, 0},       {cl.data(), cl.size() * 4, 0},
-                  {cd.data(), cd.size() * 4, 0},       {scb.data(), (size_t)D * 4, 0},
-                  {sce.data(), (size_t)D * 4, 0},      {nrep32.data(), (size_t)C * 4, 0},
+  // (dev_tables: the chunk / segment tables are k_disp_tables' outputs, only
+  // their room is reserved and nothing of them is copied)
+  const size_t nch = (size_t)std::max(n_chunks, 1);
+  Part parts[] = {{cs.data(), nch * 8, 0},               {cl.data(), nch * 4, 0},
+                  {cd.data(), nch * 4, 0},               {scb.data(), (size_t)D * 4, 0},
+                  {sce.data(), (size_t)D * 4, 0},        {nrep32.data(), (size_t)C * 4, 0},
                   {rep_idx.data(), rep_idx.size() * 4, 0},
                   {st.data(), (size_t)S * sizeof(SegState), 0},
                   {lpx.data(), (size_t)S * 8, 0}};
@@ -686,6 +704,9 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     q.off = blob;
     blob += (q.bytes + 255) & ~(size_t)255;
   }
+  // the bytes that go up: everything, or (dev_tables) nrep + rep_idx only
+  const size_t up_lo = dev_tables ? parts[5].off : 0;
+  const size_t up_hi = dev_tables ? parts[7].off : blob;
   if (!ctx->h_stage_done)
     HIP_TRY(hipEventCreateWithFlags(&ctx->h_stage_done, hipEventDisableTiming));
   else
@@ -699,9 +720,11 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   char* d_blob = (char*)scratch(ctx, "disp_tables", blob);
   if (!d_blob) return fail(H3D_ENOMEM, "disp tables");
-  for (const Part& q : parts)
-    if (q.bytes) std::memcpy((char*)ctx->h_stage + q.off, q.src, q.bytes);
-  HIP_TRY(hipMemcpyAsync(d_blob, ctx->h_stage, blob, hipMemcpyHostToDevice, s));
+  for (int qi = dev_tables ? 5 : 0; qi < (dev_tables ? 7 : 9); ++qi)
+    if (parts[qi].bytes)
+      std::memcpy((char*)ctx->h_stage + parts[qi].off, parts[qi].src, parts[qi].bytes);
+  HIP_TRY(hipMemcpyAsync(d_blob + up_lo, (char*)ctx->h_stage + up_lo, up_hi - up_lo,
+                         hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(ctx->h_stage_done, s));
   int64_t* d_cs = (int64_t*)(d_blob + parts[0].off);
   int32_t* d_cl = (int32_t*)(d_blob + parts[1].off);
@@ -726,6 +749,13 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       !d_total || !d_flags || !d_res)
     return fail(H3D_ENOMEM, "disp scratch");
   HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));
+  int* d_bad = (int*)scratch(ctx, "dist_bad", 4);
+  if (!d_bad) return fail(H3D_ENOMEM, "dist_bad");
+  if (dev_tables) {
+    const int64_t* d_seg0 = (const int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
+    hipLaunchKernelGGL(k_disp_tables, dim3(1), dim3(1024), 0, s, d_seg0, D, C, n, d_nrep,
+                       d_cs, d_cl, d_cd, d_scb, d_sce, d_st, d_lpx, d_bad);
+  }
   stamp("tables uploaded");
 
   // initial active list
@@ -756,7 +786,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     // segments are fewer than the CUs, 2 = always, 0 = one workgroup per
     // segment (k_brent)
     GangTables gang;
-    bool use_gang = ctx->brent_gang != 0 && n > 0;
+    bool use_gang = ctx->brent_gang != 0 && n > 0 && !dev_tables;
     if (use_gang) {
       int grc = mslot == 2   ? gang_setup<2>(ctx, seg_start, D, C, &gang)
                 : mslot == 4 ? gang_setup<4>(ctx, seg_start, D, C, &gang)
@@ -884,10 +914,13 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   if (rc) return rc;
   std::vector<int32_t> fl(S);
+  int bad = 0;
   HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(st.data(), d_st, S * sizeof(SegState), hipMemcpyDeviceToHost, s));
+  if (dev_tables) HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   stamp("results");
+  if (bad) return fail(H3D_EARG, "dist outside [0, %d)", D);
   int all = 0;
   for (int sg = 0; sg < S; ++sg) {
     fl[sg] = st[sg].flags;

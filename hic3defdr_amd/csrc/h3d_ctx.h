@@ -116,6 +116,9 @@ struct h3d_ctx {
   // head (0 = stream every evaluation from memory)
   int brent_lds_kb = 144;  // gang waits that timed out (fell back to k_brent)
   h3dint::TablePending tab_pending;
+  // H3D_DEV_SEG_TABLES (default 1): estimate_disp's chunk / segment tables
+  // built on the device (k_disp_tables) where no gangs are needed
+  int dev_seg_tables = 1;
   int disp_w8 = 4;  // H3D_DISP_W8: equalize register budget for M = 8
                     // (cfg4 sweep r02, ms/step W 1/2/3/4: 214/214/199/197)
 };

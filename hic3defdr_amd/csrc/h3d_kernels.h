@@ -245,6 +245,65 @@ static __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t 
   seg_start[d] = lo;
 }
 
+// The estimate_disp driver's per-call tables built on the device from the
+// segment bounds (the host built them after a sync on seg_start: ~0.1 ms of
+// idle GPU per cfg2 step): per distance its chunks of kChunk pixels
+// (chunk_start / len / distance, scanned over the distances in order), the
+// first / end chunk of each distance, every segment's initial qcml state and
+// pixel count. One 1024-thread block. *bad = 1 when a pixel's distance is
+// outside [0, D) (seg_start does not span [0, n)).
+static __global__ __launch_bounds__(1024) void k_disp_tables(
+    const int64_t* __restrict__ seg, int D, int C, int64_t n,
+    const int32_t* __restrict__ n_rep, int64_t* __restrict__ cs,
+    int32_t* __restrict__ cl, int32_t* __restrict__ cd, int32_t* __restrict__ scb,
+    int32_t* __restrict__ sce, SegState* __restrict__ st, int64_t* __restrict__ lpx,
+    int* __restrict__ bad) {
+  __shared__ int s_wsum[16];
+  __shared__ int s_carry;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_carry = 0;
+    *bad = (seg[0] != 0 || seg[D] != n) ? 1 : 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < D; base += 1024) {
+    const int d = base + threadIdx.x;
+    const int64_t len = d < D ? seg[d + 1] - seg[d] : 0;
+    const int nch = (int)((len + kChunk - 1) / kChunk);
+    int x = nch;  // inclusive scan over the block
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wsum[wid] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += (w < wid) ? s_wsum[w] : 0;
+      tot += s_wsum[w];
+    }
+    const int b0 = s_carry + before + x - nch;
+    if (d < D) {
+      scb[d] = b0;
+      sce[d] = b0 + nch;
+      const int64_t a = seg[d];
+      for (int j = 0; j < nch; ++j) {
+        cs[b0 + j] = a + (int64_t)j * kChunk;
+        cl[b0 + j] = (int32_t)min((int64_t)kChunk, len - (int64_t)j * kChunk);
+        cd[b0 + j] = d;
+      }
+      for (int c = 0; c < C; ++c) {
+        seg_init(&st[d * C + c], (long long)len, n_rep[c]);
+        lpx[d * C + c] = len;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+}
+
 // Work item w of the active list: item = chunk * C + c.
 // Equalize pass: per pixel equalize (scaled_nb.py:186-214) with the
 // segment's current dispersion, write pseudodata, then the NLL term at the

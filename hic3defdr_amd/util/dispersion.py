@@ -4,6 +4,8 @@
 - ``qcml(data, f)``: one (distance, condition) segment through the
   estimate_disp device driver (equalize + bounded Brent, k_disp_work /
   k_brent) -- the estimator ``estimate_disp(estimator='qcml')`` calls;
+  ``qcml_batch`` runs many segments in one driver call (a single-segment
+  call pays the driver's whole setup: sort, tables, launches, polls);
 - ``cml(data, f)``: one bounded-Brent search (h3d_cml);
 - ``mme_per_pixel`` / ``mme``: the per-pixel method-of-moments kernel.
 
@@ -33,6 +35,42 @@ def qcml(data, f=None, max_iter=10, tol=1e-4):
     out = ctx.disp_per_dist(data.astype(np.int64), f, np.zeros(n, np.int32),
                             np.zeros(r, np.int32), 1, 1)
     return float(out[0, 0])
+
+
+def qcml_batch(segments, max_iter=10, tol=1e-4):
+    """qcml over many segments in ONE estimate_disp driver call: ``segments``
+    is a list of (data, f) pairs as qcml takes them (f may be None); returns
+    the list of dispersions, each equal to qcml(data, f) bit for bit (every
+    segment's equalize / Brent search runs on its own pixels, in their own
+    order). The reference's estimate_disp calls qcml once per (distance,
+    condition) (analysis.py:198-246 -> dispersion.py:10-43): a caller
+    patching that loop gathers its segments first and makes this one call
+    instead of several hundred single-segment driver runs."""
+    if tol != 1e-4:
+        raise NotImplementedError('the device qcml converges at tol=1e-4')
+    out = [np.nan] * len(segments)
+    by_r = {}
+    for i, (data, f) in enumerate(segments):
+        data = np.asarray(data)
+        if data.ndim != 2:
+            raise ValueError('data must be (pixels, replicates)')
+        if data.size and not np.all(data == np.floor(data)):
+            raise ValueError('qcml takes integer counts')
+        n, r = data.shape
+        f = np.ones((n, r)) if f is None else np.broadcast_to(f, (n, r))
+        by_r.setdefault(r, []).append((i, data, f))
+    ctx = _native.context()
+    for r, group in by_r.items():
+        # one pseudo-distance per segment, one condition of r replicates
+        raw = np.concatenate([d for _, d, _ in group]).astype(np.int64)
+        ff = np.concatenate([f for _, _, f in group]).astype(np.float64)
+        dist = np.concatenate([np.full(len(d), j, np.int32)
+                               for j, (_, d, _) in enumerate(group)])
+        res = ctx.disp_per_dist(raw.reshape(-1, r), ff.reshape(-1, r), dist,
+                                np.zeros(r, np.int32), 1, len(group))
+        for j, (i, _, _) in enumerate(group):
+            out[i] = float(res[j, 0])
+    return out
 
 
 def cml(data, f=None):

@@ -44,3 +44,32 @@ def test_dispersion_operators_match_reference():
         assert rel_err(dispersion.mme(y, f=f.copy()), g['seg%d_mme' % s]) < 1e-12
     with pytest.raises(Exception):
         dispersion.cml(g['seg0_data'].copy(), f=g['seg0_f'])  # int /= float
+
+
+def test_qcml_batch_equals_per_segment_calls():
+    """qcml_batch: every segment in one driver call, bit-equal to the
+    single-segment qcml calls (and to the reference's values); the per-call
+    and batched costs printed (-rP) for INTEGRATION.md."""
+    import time
+    from hic3defdr_amd.synthetic import draw_band
+    from hic3defdr_amd.util import dispersion
+    g = golden('unit_nb.npz')
+    segs = [(g['seg%d_data' % s], g['seg%d_f' % s])
+            for s in range(int(g['n_segs']))]
+    # plus the segments of a synthetic band: (distance, condition) blocks
+    raw, f, dist = draw_band(2000, (2, 3), 60, seed=9)
+    for d in range(4, 61, 3):
+        m = dist == d
+        segs += [(raw[m][:, :2], f[m][:, :2]), (raw[m][:, 2:], f[m][:, 2:])]
+    batched = dispersion.qcml_batch(segs)
+    t0 = time.perf_counter()
+    single = [dispersion.qcml(d, f=ff) for d, ff in segs]
+    t1 = time.perf_counter()
+    dispersion.qcml_batch(segs)
+    t2 = time.perf_counter()
+    np.testing.assert_array_equal(np.array(batched), np.array(single))
+    for s in range(int(g['n_segs'])):
+        assert rel_err(batched[s], g['seg%d_qcml' % s]) < 1e-6
+    print('qcml: %d segments, %.2f ms per single-segment call, %.2f ms for '
+          'the batch' % (len(segs), (t1 - t0) / len(segs) * 1e3,
+                         (t2 - t1) * 1e3))

@@ -16,9 +16,9 @@ done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
   -d gpurun_out/${tag}_prof -o run -- python3 -u bench.py --no-cpu-baseline --no-e2e --steps 5 \
   > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err
-f=$(find gpurun_out/${tag}_prof -name '*kernel_trace.csv' | head -n 1)
+f=$(find gpurun_out/${tag}_prof -name '*kernel_trace.csv' -print -quit)
 python3 tools/trace_gaps.py $f 15 > gpurun_out/${tag}_trace_gaps.txt
-s=$(find gpurun_out/${tag}_prof -name '*kernel_stats.csv' | head -n 1)
+s=$(find gpurun_out/${tag}_prof -name '*kernel_stats.csv' -print -quit)
 cp $s gpurun_out/${tag}_kernel_stats.csv
 rm -rf gpurun_out/${tag}_prof
 cat gpurun_out/${tag}_trace_gaps.txt | head -n 30

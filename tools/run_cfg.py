@@ -77,15 +77,17 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
+    from bench import table_lrt   # the bench step's table -> LRT
+    tl = table_lrt(torch, dev, ctx, D, C)
+    o = {'p': t_p, 'llr': t_llr, 'mu0': t_m0, 'mu1': t_m1, 'disp': t_disp}
+
     def step():
         dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                     t_d.data_ptr(), n, R, cond, C, D)
-        tab = _native.disp_tables(dpd)
-        ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), tab, n,
-                    R, cond, t_p.data_ptr(), t_llr.data_ptr(),
-                    t_m0.data_ptr(), t_m1.data_ptr(), t_disp.data_ptr())
+        tl(dpd, t_raw, t_f, t_d, n, R, cond, o)
         return dpd
 
+    first = None
     for _ in range(args.warmup):
         first = step()
     torch.cuda.synchronize()
@@ -115,8 +117,8 @@ def main():
                 dpd[present]))),
             'disp_nan_where_absent': bool(np.all(np.isnan(dpd[~present]))),
             'p_in_0_1': bool(np.all((p >= 0) & (p <= 1))),
-            'deterministic_disp': bool(np.array_equal(first, dpd,
-                                                      equal_nan=True)),
+            'deterministic_disp': None if first is None else bool(
+                np.array_equal(first, dpd, equal_nan=True)),
             'frac_p_lt_0.05': float(np.mean(p < 0.05))},
         'generate_s': gen_s,
     }
