@@ -6,7 +6,8 @@ Workloads (BASELINE.json configs):
   generator, seed = rank). Untimed setup: generate the input files, run the
   product's GPU prepare_data, upload raw / f / dist of the disp pixels to
   HBM. One step = estimate_disp (qcml per distance x condition) + the lowess
-  smoothing tables (on the GPU, h3d_disp_tables_dev; H3D_DEV_TABLE=0 for the
+  smoothing tables (on the GPU from estimate_disp's result in place,
+  h3d_estimate_disp_dev; H3D_DEV_TABLE=1 / 0 for the separate device / the
   host smoother) + lrt (fused per-pixel GLM fits + LRT) on the resident
   inputs, outputs left in HBM.
 - cfg3 (configs[2], the N > 1 default; --config cfg3 at any N): the whole
@@ -335,31 +336,55 @@ def _upload(torch, dev, raw, f, dist_np):
 
 
 def table_lrt(torch, dev, ctx, D, C):
-    """The step's dispersion table -> LRT: on the device (h3d_disp_tables_dev
-    then h3d_lrt_dev_tab: the per-distance estimates go up once, the smoother
-    runs on the GPU, nothing waits in between) unless H3D_DEV_TABLE=0, which
-    keeps the host smoother (h3d_disp_tables) and uploads its table."""
+    """The step's dispersion table -> LRT. H3D_DEV_TABLE=2 (default): the
+    smoother runs on the device from estimate_disp's result in place
+    (h3d_estimate_disp_dev, then h3d_lrt_dev_tab) -- use `.estimate` for the
+    estimate_disp of the step; 1: the device smoother on an uploaded table
+    (h3d_disp_tables_dev); 0: the host smoother (h3d_disp_tables) and an
+    uploaded table. Callers whose table comes from elsewhere (the distance
+    re-shard's all-reduce, the emulation's filled rows) call the object
+    with it; `estimate` falls back to that path when the mode is not 2."""
     from hic3defdr_amd import _native
-    use_dev = os.environ.get('H3D_DEV_TABLE', '1') != '0' and \
-        hasattr(ctx.lib, 'h3d_disp_tables_dev')
+    mode = int(os.environ.get('H3D_DEV_TABLE', '2'))
+    if mode >= 1 and not hasattr(ctx.lib, 'h3d_disp_tables_dev'):
+        mode = 0
+    if mode == 2 and not hasattr(ctx.lib, 'h3d_estimate_disp_dev'):
+        mode = 1
     pin = torch.empty((D, C), dtype=torch.float64).pin_memory()
     t_dpd = torch.empty((D, C), dtype=torch.float64, device=dev)
     t_tab = torch.empty_like(t_dpd)
+    fused = {'ready': False}
+
+    def ptrs(o):
+        return (o['p'].data_ptr(), o['llr'].data_ptr(), o['mu0'].data_ptr(),
+                o['mu1'].data_ptr(), o['disp'].data_ptr())
+
+    def estimate(t_raw, t_f, t_dist, n, R, cond):
+        if mode == 2:
+            fused['ready'] = True
+            return ctx.estimate_disp_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                         t_dist.data_ptr(), n, R, cond, C, D,
+                                         t_tab.data_ptr())
+        return ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                     t_dist.data_ptr(), n, R, cond, C, D)
 
     def run(dpd, t_raw, t_f, t_dist, n, R, cond, o):
-        ptrs = (o['p'].data_ptr(), o['llr'].data_ptr(), o['mu0'].data_ptr(),
-                o['mu1'].data_ptr(), o['disp'].data_ptr())
-        if use_dev:
+        if fused['ready']:       # the tables of this dpd are on the device
+            fused['ready'] = False
+            ctx.lrt_dev_tab(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
+                            t_tab.data_ptr(), D, n, R, cond, *ptrs(o))
+        elif mode >= 1:
             pin.numpy()[...] = dpd
             t_dpd.copy_(pin, non_blocking=True)   # the ctx's stream
             ctx.disp_tables_dev(t_dpd.data_ptr(), D, C, t_tab.data_ptr())
             ctx.lrt_dev_tab(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
-                            t_tab.data_ptr(), D, n, R, cond, *ptrs)
+                            t_tab.data_ptr(), D, n, R, cond, *ptrs(o))
         else:
             tab = _native.disp_tables(dpd)
             ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
-                        tab, n, R, cond, *ptrs)
-    run.on_device = use_dev
+                        tab, n, R, cond, *ptrs(o))
+    run.estimate = estimate
+    run.mode = mode
     return run
 
 
@@ -532,6 +557,8 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
             if by_dist:
                 dpd = parallel.disp_per_dist_by_distance(
                     ctx, t_raw, t_f, t_dist, cond, C, D)
+            elif reduce is None:
+                dpd = tl.estimate(t_raw, t_f, t_dist, n, R, cond)
             else:
                 dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
                                             t_dist.data_ptr(), n, R, cond, C,
@@ -640,8 +667,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
                 dpd[gap, c] = np.interp(gi, np.flatnonzero(fin), dpd[fin, c]) \
                     * (1 + 0.02 * np.sin(1.7 * gi + c))
         else:
-            dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
-                                        t_dist.data_ptr(), n, R, cond, C, D)
+            dpd = tl.estimate(t_raw, t_f, t_dist, n, R, cond)
         tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
         if world > 1:
             o['q'] = parallel.bh_all_ranks(o['p'], bh_fn)

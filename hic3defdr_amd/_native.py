@@ -31,12 +31,14 @@ EXPORTS = [
     'h3d_lrt_poisson_dev', 'h3d_mme_per_pixel', 'h3d_lrt_wide', 'h3d_cml',
     'h3d_bh_ctx', 'h3d_bh_dev', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
     'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
+    'h3d_estimate_disp_dev',
 ]
 
 
 # entry points a library built from an older tree may lack; callers check
 OPTIONAL = ('h3d_disp_tables', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
-            'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab')
+            'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
+            'h3d_estimate_disp_dev')
 
 
 class H3DError(RuntimeError):
@@ -117,6 +119,8 @@ def load_library(path=None):
             'h3d_cml': (_I, [_P, _P, _I64, _I, _P]),
             'h3d_disp_tables_dev': (_I, [_P, _P, _I, _I, _I, _D, _D, _P]),
             'h3d_disp_tables_wait': (_I, [_P]),
+            'h3d_estimate_disp_dev': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I,
+                                           _I, _D, _D, _P, _P, _P]),
             'h3d_lrt_dev_tab': (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _I,
                                      _I, _P, _P, _P, _P, _P]),
             'h3d_npz_csr_info': (_I, [ctypes.c_char_p, _P, _P, _P]),
@@ -398,6 +402,22 @@ class Context(object):
             self.handle, d_dpd, D, C, int(bool(weighted)),
             -1.0 if frac is None else float(frac), float(auto_frac_factor),
             d_tables), 'h3d_disp_tables_dev')
+
+    def estimate_disp_dev(self, d_raw, d_f, d_dist, n, R, cond_of_rep, C, D,
+                          d_tables, weighted=True, frac=None,
+                          auto_frac_factor=15.):
+        """disp_per_dist_dev whose smoothed (D, C) tables are computed on
+        the device into ``d_tables`` (settled by lrt_dev_tab /
+        disp_tables_wait); returns disp_per_dist on the host."""
+        cond = _c(cond_of_rep, np.int32)
+        out = np.empty((D, C), dtype=np.float64)
+        flags = np.zeros((D, C), dtype=np.int32)
+        _check(self.lib.h3d_estimate_disp_dev(
+            self.handle, d_raw, d_f, d_dist, n, R, C, _ptr(cond), D,
+            int(bool(weighted)), -1.0 if frac is None else float(frac),
+            float(auto_frac_factor), _ptr(out), _ptr(flags), d_tables),
+            'h3d_estimate_disp_dev')
+        return out
 
     def disp_tables_wait(self):
         _check(self.lib.h3d_disp_tables_wait(self.handle),

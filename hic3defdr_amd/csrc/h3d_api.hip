@@ -473,11 +473,48 @@ int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
 // estimate_disp
 // ---------------------------------------------------------------------------
 
+namespace {
+// h3d_estimate_disp_dev's request: the smoothed tables of the result, on the
+// device, enqueued behind the result copies
+struct TableReq {
+  int weighted;
+  double frac, aff;
+  double* d_tables;
+};
+
+int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                       const int32_t* d_dist, int64_t n, int R, int C,
+                       const int32_t* cond_of_rep, int D, int estimator,
+                       double* disp_per_dist, int32_t* seg_flags_out,
+                       h3d_allreduce_fn reduce, void* user, const TableReq* treq);
+}  // namespace
+
 int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                           const int32_t* d_dist, int64_t n, int R, int C,
                           const int32_t* cond_of_rep, int D, int estimator,
                           double* disp_per_dist, int32_t* seg_flags_out,
                           h3d_allreduce_fn reduce, void* user) {
+  return disp_per_dist_core(ctx, d_raw, d_f, d_dist, n, R, C, cond_of_rep, D, estimator,
+                            disp_per_dist, seg_flags_out, reduce, user, nullptr);
+}
+
+int h3d_estimate_disp_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                          const int32_t* d_dist, int64_t n, int R, int C,
+                          const int32_t* cond_of_rep, int D, int weighted, double frac,
+                          double auto_frac_factor, double* disp_per_dist,
+                          int32_t* seg_flags_out, double* d_tables_out) {
+  if (!d_tables_out) return fail(H3D_EARG, "null d_tables_out");
+  const TableReq req{weighted, frac, auto_frac_factor, d_tables_out};
+  return disp_per_dist_core(ctx, d_raw, d_f, d_dist, n, R, C, cond_of_rep, D, H3D_EST_QCML,
+                            disp_per_dist, seg_flags_out, nullptr, nullptr, &req);
+}
+
+namespace {
+int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                       const int32_t* d_dist, int64_t n, int R, int C,
+                       const int32_t* cond_of_rep, int D, int estimator,
+                       double* disp_per_dist, int32_t* seg_flags_out,
+                       h3d_allreduce_fn reduce, void* user, const TableReq* treq) {
   if (!ctx || !cond_of_rep || !disp_per_dist) return fail(H3D_EARG, "null argument");
   if (n < 0 || D < 1) return fail(H3D_EARG, "n=%lld D=%d", (long long)n, D);
   if (n > 0 && (!d_raw || !d_f || !d_dist)) return fail(H3D_EARG, "null device input");
@@ -918,7 +955,20 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(st.data(), d_st, S * sizeof(SegState), hipMemcpyDeviceToHost, s));
   if (dev_tables) HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (treq) {
+    // the smoother runs behind the result copies; the host waits for the
+    // copies only, so the kernel overlaps the return to the caller
+    hipEvent_t copied = ev_get(ctx);
+    HIP_TRY(hipEventRecord(copied, s));
+    const int trc = h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac,
+                                        treq->aff, treq->d_tables);
+    const hipError_t e = hipEventSynchronize(copied);
+    ctx->event_pool.push_back(copied);
+    if (trc) return trc;
+    if (e != hipSuccess) return fail(H3D_EHIP, "result copy: %s", hipGetErrorString(e));
+  } else {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
   stamp("results");
   if (bad) return fail(H3D_EARG, "dist outside [0, %d)", D);
   int all = 0;
@@ -929,6 +979,7 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   if (seg_flags_out) std::memcpy(seg_flags_out, fl.data(), S * 4);
   return flags_to_code(all);
 }
+}  // namespace
 
 int h3d_disp_per_dist(h3d_ctx* ctx, const int64_t* raw, const double* f,
                       const int32_t* dist, int64_t n, int R, int C,

@@ -178,6 +178,21 @@ int h3d_disp_tables_dev(h3d_ctx* ctx, const double* d_disp_per_dist, int D,
                         double auto_frac_factor, double* d_tables_out);
 int h3d_disp_tables_wait(h3d_ctx* ctx);
 
+/* estimate_disp (qcml, h3d_disp_per_dist_dev without a reduce) whose
+ * smoothed tables are computed on the device from the result in place
+ * (analysis.py:198-246 then :226-240): disp_per_dist (D, C) on the host as
+ * h3d_disp_per_dist_dev returns it, the tables into d_tables_out (device,
+ * (D, C)), the smoother running while the call returns. Settled like
+ * h3d_disp_tables_dev; it reads the ctx's result buffer, so the next
+ * estimate_disp call on the ctx must come after h3d_lrt_dev_tab /
+ * h3d_disp_tables_wait. */
+int h3d_estimate_disp_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
+                          const int32_t* d_dist, int64_t n, int R, int C,
+                          const int32_t* cond_of_rep, int D, int weighted,
+                          double frac, double auto_frac_factor,
+                          double* disp_per_dist, int32_t* seg_flags,
+                          double* d_tables_out);
+
 /* ---- lrt --------------------------------------------------------------- */
 
 /* Per-pixel LRT (lrt.py:7-50) with disp[i, c] = disp_table[dist[i], c]

@@ -138,3 +138,36 @@ def test_lrt_over_device_table(ctx):
     np.testing.assert_array_equal(t_tab.cpu().numpy(), host_tab)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+
+
+def test_fused_estimate_disp_tables(ctx):
+    """h3d_estimate_disp_dev: the same disp_per_dist as h3d_disp_per_dist_dev,
+    the host smoother's tables on the device, the same LRT."""
+    import torch
+    from hic3defdr_amd.synthetic import draw_band
+    raw, f, dist = draw_band(3000, (2, 3), 60, seed=6)
+    n, R = raw.shape
+    cond = np.array([0, 0, 1, 1, 1], dtype=np.int32)
+    C, D = 2, 61
+    dev = torch.device('cuda', 0)
+    t_raw = torch.from_numpy(raw.astype(np.int32)).to(dev)
+    t_f = torch.from_numpy(f).to(dev)
+    t_d = torch.from_numpy(dist.astype(np.int32)).to(dev)
+    t_tab = torch.full((D, C), -7.0, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ref = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                t_d.data_ptr(), n, R, cond, C, D)
+    got = ctx.estimate_disp_dev(t_raw.data_ptr(), t_f.data_ptr(),
+                                t_d.data_ptr(), n, R, cond, C, D,
+                                t_tab.data_ptr())
+    np.testing.assert_array_equal(got, ref)
+    outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
+    outs += [torch.empty((n, C), dtype=torch.float64, device=dev)
+             for _ in range(2)]
+    ctx.lrt_dev_tab(t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(),
+                    t_tab.data_ptr(), D, n, R, cond,
+                    *[x.data_ptr() for x in outs])
+    np.testing.assert_array_equal(t_tab.cpu().numpy(), _host_tables(ref))
+    p_host = ctx.lrt(raw.astype(np.int64), f, dist,
+                     _host_tables(ref), cond)[0]
+    np.testing.assert_array_equal(outs[0].cpu().numpy(), p_host)

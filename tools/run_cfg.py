@@ -82,8 +82,7 @@ def main():
     o = {'p': t_p, 'llr': t_llr, 'mu0': t_m0, 'mu1': t_m1, 'disp': t_disp}
 
     def step():
-        dpd = ctx.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
-                                    t_d.data_ptr(), n, R, cond, C, D)
+        dpd = tl.estimate(t_raw, t_f, t_d, n, R, cond)
         tl(dpd, t_raw, t_f, t_d, n, R, cond, o)
         return dpd
 
