@@ -18,7 +18,8 @@ Workloads (BASELINE.json configs):
   distance re-shard: distances LPT-assigned by pixel count, one all_to_all
   of the disp pixels, the single-GPU driver per rank, one all-reduce of the
   D x C table) + lowess tables + lrt of the rank's own pixels + the
-  genome-wide BH (one all_gather of the p-values, the GPU BH on every rank).
+  genome-wide BH (parallel.bh_sharded: a sample sort of the p-values over
+  the ranks, each rank ranking one value range on its GPU).
 
 The CPU baseline (rank 0, N = 1, cfg2) runs FIRST, before anything touches
 the GPU (its worker pool forks): the CPU restatement (oracle/, numpy/scipy)
@@ -614,8 +615,10 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
     if emu:
         own = [p for i, p in enumerate(parts) if i in mine]
         d_all = np.concatenate([p[2] for p in parts])
-        owner = parallel.distance_owners(
-            np.bincount(d_all, minlength=D)[:D], e_world)
+        d_cnt = np.bincount(d_all, minlength=D)[:D]
+        owner = parallel.distance_owners(d_cnt, e_world)
+        # the rank's live segments, as disp_per_dist_by_distance hints them
+        e_live = int(((owner == e_rank) & (d_cnt > 0)).sum()) * 2
         keep = owner[d_all] == e_rank
         e_raw = np.concatenate([p[0] for p in parts])[keep]
         e_f = np.concatenate([p[1] for p in parts])[keep]
@@ -642,10 +645,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
-    def bh_fn(t):
-        q = torch.empty_like(t)
-        ctx.bh_dev(t.data_ptr(), t.numel(), q.data_ptr())
-        return q
+    bh_ops = parallel.DeviceBhOps(ctx)
 
     tl = table_lrt(torch, dev, ctx, D, C)
 
@@ -654,6 +654,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
             dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
                                                      cond, C, D)
         elif emu:
+            ctx.set_live_hint(e_live)
             dpd = ctx.disp_per_dist_dev(te_raw.data_ptr(), te_f.data_ptr(),
                                         te_dist.data_ptr(), e_n, R, cond, C, D)
             # the other ranks' rows (not run here): interpolated over this
@@ -670,7 +671,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
             dpd = tl.estimate(t_raw, t_f, t_dist, n, R, cond)
         tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
         if world > 1:
-            o['q'] = parallel.bh_all_ranks(o['p'], bh_fn)
+            o['q'] = parallel.bh_sharded(o['p'], bh_ops)
         else:
             ctx.bh_dev(o['p'].data_ptr(), n, o['q'].data_ptr())
         return dpd
@@ -689,8 +690,9 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
         'dp%d: %s' % (world, 'one GPU' if world == 1 else
                       'distance re-shard (LPT distance owners, all_to_all of '
                       'the disp pixels, single-GPU driver per rank, table '
-                      'all-reduce), LRT on own chromosomes, BH over one '
-                      'all_gather of the p-values'), 'strong')
+                      'all-reduce), LRT on own chromosomes, genome-wide BH '
+                      'as a sample sort over the ranks (two all_to_alls of '
+                      'the p-values)'), 'strong')
     out['config']['chromosomes_rank0'] = [int(i) for i in mine]
     out['config']['generate_s_rank0'] = gen_s
     if emu:
@@ -699,7 +701,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
             'note': 'one rank\'s share of an N-GPU cfg3 run, timed alone on '
                     'one GPU: estimate_disp over its LPT-owned distances, lrt '
                     '+ BH over its LPT-owned chromosomes; no collectives (the '
-                    'all_to_all, table all-reduce and p all_gather are not '
+                    'all_to_all, table all-reduce and BH exchanges are not '
                     'run). value = its pixels / time, NOT a scaling number'}
     return out
 

@@ -294,8 +294,8 @@ class AnalyzingHiC3DeFDR(object):
                 li = self.load_data('loop_idx', chrom) \
                     if self.loop_patterns else None
                 mine[chrom] = self.load_data('pvalues', chrom, idx=li)
-            for chrom, q in parallel.distributed_bh(sh, mine,
-                                                    self._ctx().bh).items():
+            for chrom, q in parallel.distributed_bh(
+                    sh, mine, ctx=self._ctx()).items():
                 self.save_data(q, 'qvalues', chrom)
             sh.barrier()
             return

@@ -111,10 +111,13 @@ struct h3d_ctx {
   // H3D_BRENT: 1 = gang Brent searches (k_brent_gang) where one workgroup
   // per segment leaves CUs idle, 2 = always, 0 = k_brent only
   int brent_gang = 1;
-  int gang_aborts = 0;
+  int gang_aborts = 0;  // gang waits that timed out (fell back to k_brent)
   // H3D_BRENT_LDS_KB: LDS per k_brent workgroup for the segment's staged
   // head (0 = stream every evaluation from memory)
-  int brent_lds_kb = 144;  // gang waits that timed out (fell back to k_brent)
+  int brent_lds_kb = 144;
+  // h3d_set_live_hint: (distance, condition) segments with pixels in the
+  // next estimate_disp call as the caller knows them (0 = unknown: all D x C)
+  int64_t live_hint = 0;
   h3dint::TablePending tab_pending;
   // H3D_DEV_SEG_TABLES (default 1): estimate_disp's chunk / segment tables
   // built on the device (k_disp_tables) where no gangs are needed

@@ -5,8 +5,8 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI;
 itself (``Shards``): every rank prepares and tests its own chromosomes and
 writes their outdir files (one shared outdir, as the reference's per-
 chromosome processes do); estimate_disp keeps the genome-wide pooling by a
-re-shard by distance; BH runs genome-wide on every rank over all-gathered
-p-values (``distributed_bh``).
+re-shard by distance; BH runs genome-wide as a sample sort of the p-values
+over the ranks (``bh_sharded``).
 
 * prepare_data and lrt are independent per chromosome: chromosomes are
   assigned to ranks by greedy longest-processing-time on pixel counts
@@ -23,11 +23,15 @@ p-values (``distributed_bh``).
   owns, and one all-reduce of the D x C table (owners' rows, zeros
   elsewhere) gives every rank the same disp_per_dist. The only change from
   one GPU is the order of each segment's pixels (ULP-level).
-* BH (``distributed_bh`` / ``bh_all_ranks``): one all_gather of the
-  p-values (tensors on the rank's GPU under nccl); every rank runs the same
-  genome-wide BH on the gathered vector and keeps its own slice. BH's
-  q-values do not depend on the order of the p-values (tied p-values share
-  one q), so rank order instead of chromosome order changes no bit.
+* BH (``bh_sharded``, used by ``distributed_bh`` and bench): each rank
+  sorts its p-values, ships each to the rank owning its value range, ranks
+  its bucket globally from the bucket sizes and completes the reverse
+  minimum with the higher buckets' minima -- O(n / world) sort work per rank
+  and two all_to_alls of one double per p-value, instead of every rank
+  sorting the whole genome's p-values; bit-identical to one process' BH
+  (tied p-values share one q, so neither the rank order nor the order
+  inside a tie changes a bit). ``bh_all_ranks`` (all_gather + one BH of
+  everything on every rank) remains for host BH functions.
 * The per-pass alternative (``make_allreduce``, H3D_DISP_SHARD=pass) keeps
   the pixels in place and all-reduces the per-(distance, condition) NLL sums
   of every Brent step (D x C doubles, ~3 KB, ~54 passes per cfg2
@@ -140,6 +144,11 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
         raw_m = torch.empty((0, R), dtype=torch.int32, device=dev)
         f_m = torch.empty((0, R), dtype=torch.float64, device=dev)
         dist_m = torch.empty(0, dtype=torch.int32, device=dev)
+    # this rank's live segments (its owned distances with pixels): with fewer
+    # than the CUs the driver splits each Brent search over a gang
+    if hasattr(ctx, 'set_live_hint'):
+        own = (owner_of == rank) & (cnt.cpu().numpy() > 0)
+        ctx.set_live_hint(max(1, int(own.sum()) * C))
     tab = ctx.disp_per_dist_dev(raw_m.data_ptr(), f_m.data_ptr(),
                                 dist_m.data_ptr(), m, R, cond_of_rep, C, D)
     tab[owner_of != rank] = 0.0
@@ -256,20 +265,162 @@ def bh_all_ranks(t_p, bh_fn, group=None):
     return bh_fn(allp)[off:off + t_p.numel()]
 
 
-def distributed_bh(shards, pvalues, bh):
+class DeviceBhOps(object):
+    """bh_sharded's per-rank compute on the rank's GPU (libh3d's
+    h3d_bh_sort_dev / _scan_dev / _finish_dev, tensors on the ctx's
+    device). The ctx may run on its own stream: torch's current stream is
+    drained before each call (its tensors are the inputs), and each call
+    returns with the ctx stream drained."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def _ready(self, t):
+        import torch
+        torch.cuda.current_stream(t.device).synchronize()
+
+    def sort(self, keys, vals=None):
+        """(keys ascending with non-finite last, their values -- the given
+        ones or the positions --, number of finite keys)."""
+        import torch
+        keys = keys.contiguous()
+        self._ready(keys)
+        n = keys.numel()
+        ko = torch.empty_like(keys)
+        vo = torch.empty(n, dtype=torch.int64, device=keys.device)
+        m = self.ctx.bh_sort_dev(keys.data_ptr(),
+                                 None if vals is None else vals.data_ptr(),
+                                 n, ko.data_ptr(), vo.data_ptr())
+        return ko, vo, m
+
+    def scan(self, ps, offset, m):
+        """(suffix minimum of the BH ratios of a sorted bucket at global
+        ranks offset.., its first entry)."""
+        import torch
+        sc = torch.empty_like(ps)
+        self._ready(ps)
+        lo = self.ctx.bh_scan_dev(ps.data_ptr(), ps.numel(), offset, m,
+                                  sc.data_ptr())
+        return sc, lo
+
+    def finish(self, scanned, higher_min):
+        import torch
+        q = torch.empty_like(scanned)
+        self._ready(scanned)
+        self.ctx.bh_finish_dev(scanned.data_ptr(), scanned.numel(),
+                               higher_min, q.data_ptr())
+        return q
+
+
+def bh_sharded(t_p, ops, group=None, samples=64):
+    """Genome-wide BH over every rank's p-values `t_p` (1-D float64 tensor),
+    each rank computing the q-values of one VALUE range (a sample sort)
+    instead of every rank sorting all of them: returns this rank's q (same
+    order as `t_p`), bit-identical to the single-process BH of all ranks'
+    p-values concatenated (reference analysis.py:286-303; q of NaN p is
+    NaN and NaN p are not counted).
+
+    1. each rank sorts its p-values (ops.sort) and contributes `samples`
+       evenly spaced order statistics + its finite count to one all_gather;
+       every rank derives the same world - 1 splitters (count-weighted
+       quantiles), so equal values always land in one bucket;
+    2. one all_gather of every rank's per-bucket counts (global offsets),
+       one all_to_all of the values to their bucket's rank;
+    3. the bucket is sorted, its ratios p_(j) / ((offset + j + 1) / m)
+       min-scanned from the top (ops.scan), one all_gather of the bucket
+       minima completes the reverse minimum across buckets (ops.finish);
+    4. one all_to_all returns each q to the rank (and position) it came
+       from.
+    `ops`: DeviceBhOps (the GPU) or a host stand-in with the same methods."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = t_p.device
+    xdev = _xdev(dev, group)
+    n = t_p.numel()
+    ks, idx, m_loc = ops.sort(t_p.to(torch.float64))
+    fin = ks[:m_loc]
+    # 1. splitters
+    if m_loc:
+        pos = torch.div(torch.arange(samples, device=dev) * m_loc, samples,
+                        rounding_mode='floor')
+        smp = fin[pos]
+    else:
+        smp = torch.full((samples,), float('inf'), dtype=torch.float64,
+                         device=dev)
+    meta = torch.cat([smp, torch.tensor([float(m_loc)], dtype=torch.float64,
+                                        device=dev)]).to(xdev)
+    got = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(got, meta, group=group)
+    g = torch.stack(got).cpu().numpy()
+    cnt = g[:, -1]
+    sv = g[:, :-1].ravel()
+    sw = np.repeat(cnt / samples, samples)
+    keep = sw > 0
+    sv, sw = sv[keep], sw[keep]
+    o = np.argsort(sv, kind='stable')
+    sv, cw = sv[o], np.cumsum(sw[o])
+    if len(sv):
+        at = np.searchsorted(cw, cw[-1] * np.arange(1, world) / world)
+        split = sv[np.minimum(at, len(sv) - 1)]
+    else:
+        split = np.full(world - 1, np.inf)
+    # 2. bucket b = (split[b - 1], split[b]]
+    cut = torch.searchsorted(fin, torch.from_numpy(split).to(dev),
+                             right=True).tolist() if world > 1 else []
+    bounds = [0] + [int(c) for c in cut] + [m_loc]
+    send = [bounds[b + 1] - bounds[b] for b in range(world)]
+    st = torch.tensor(send, dtype=torch.int64, device=xdev)
+    sends = [torch.empty_like(st) for _ in range(world)]
+    dist.all_gather(sends, st, group=group)
+    table = np.stack([s.cpu().numpy() for s in sends])   # [src, bucket]
+    recv = [int(v) for v in table[:, rank]]
+    sizes = table.sum(axis=0)
+    offset, m = int(sizes[:rank].sum()), int(sizes.sum())
+    mb = int(sizes[rank])
+    got_p = torch.empty(mb, dtype=torch.float64, device=xdev)
+    dist.all_to_all_single(got_p, fin.to(xdev), output_split_sizes=recv,
+                           input_split_sizes=send, group=group)
+    # 3. the bucket's q
+    bs, perm, _ = ops.sort(got_p.to(dev))
+    sc, lo = ops.scan(bs, offset, m)
+    lt = torch.tensor([lo], dtype=torch.float64, device=xdev)
+    los = [torch.empty_like(lt) for _ in range(world)]
+    dist.all_gather(los, lt, group=group)
+    higher = min([float(v.item()) for v in los[rank + 1:]] or [float('inf')])
+    q_sorted = ops.finish(sc, higher)
+    # 4. back in received order, then to the senders
+    q_recv = torch.empty_like(q_sorted)
+    q_recv[perm] = q_sorted
+    back = torch.empty(m_loc, dtype=torch.float64, device=xdev)
+    dist.all_to_all_single(back, q_recv.to(xdev), output_split_sizes=send,
+                           input_split_sizes=recv, group=group)
+    q = torch.full((n,), float('nan'), dtype=torch.float64, device=dev)
+    q[idx[:m_loc]] = back.to(dev)
+    return q
+
+
+def distributed_bh(shards, pvalues, bh=None, ctx=None):
     """Genome-wide BH over every rank's p-values (analysis.py:286-303 over
-    all chromosomes): ``pvalues`` maps this rank's chromosomes to arrays;
-    ``bh`` maps a numpy vector to its q-values. Returns this rank's
-    chromosomes' q-values (dict)."""
+    all chromosomes): ``pvalues`` maps this rank's chromosomes to arrays.
+    With ``ctx`` (the product): ``bh_sharded`` on the rank's GPU; else
+    ``bh`` maps a numpy vector to its q-values and runs on all-gathered
+    p-values. Returns this rank's chromosomes' q-values (dict)."""
     import torch
     dist = shards.dist
     mine = [c for c in shards.mine if c in pvalues]
     local = np.concatenate([np.asarray(pvalues[c], dtype=np.float64)
                             for c in mine]) if mine else np.zeros(0)
-    dev = torch.device('cuda', torch.cuda.current_device()) \
-        if dist.get_backend() == 'nccl' else torch.device('cpu')
-    q = bh_all_ranks(torch.from_numpy(local).to(dev),
-                     lambda t: torch.from_numpy(bh(t.cpu().numpy())))
+    if ctx is not None:
+        gdev = torch.device('cuda', ctx.device)
+        q = bh_sharded(torch.from_numpy(local).to(gdev), DeviceBhOps(ctx))
+    else:
+        dev = torch.device('cuda', torch.cuda.current_device()) \
+            if dist.get_backend() == 'nccl' else torch.device('cpu')
+        q = bh_all_ranks(torch.from_numpy(local).to(dev),
+                         lambda t: torch.from_numpy(bh(t.cpu().numpy())))
     q = q.cpu().numpy()
     off = np.concatenate([[0], np.cumsum([len(pvalues[c]) for c in mine])])
     return {c: q[off[i]:off[i + 1]] for i, c in enumerate(mine)}

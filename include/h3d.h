@@ -86,6 +86,16 @@ void h3d_close(h3d_ctx* ctx);
 const char* h3d_last_error(void);
 /* stream the ctx launches on (hipStream_t); NULL = the ctx's own stream */
 int h3d_set_stream(h3d_ctx* ctx, void* stream);
+/* The number of (distance, condition) segments that hold pixels in the NEXT
+ * h3d_disp_per_dist[_dev] / h3d_estimate_disp_dev call, when the caller
+ * knows it (0 = unknown: D x C); consumed by that call. A rank of the
+ * multi-GPU distance re-shard owns ~D / world distances: with fewer live
+ * segments than CUs the driver runs each Brent search over several
+ * workgroups (gangs), which needs the segment bounds on the host, instead of
+ * building its tables on the device without a host sync. Multi-GPU
+ * addition, no reference counterpart (analysis.py:169-206 pools every
+ * distance in one process). */
+int h3d_set_live_hint(h3d_ctx* ctx, int64_t live_segments);
 
 /* ---- prepare_data ------------------------------------------------------ */
 
@@ -246,6 +256,26 @@ int h3d_bh(const double* p, int64_t n, double* q);
  * ordered on the ctx stream (n < 2^31). */
 int h3d_bh_ctx(h3d_ctx* ctx, const double* p, int64_t n, double* q);
 int h3d_bh_dev(h3d_ctx* ctx, const double* d_p, int64_t n, double* d_q);
+
+/* The same BH over p-values sharded across ranks (analysis.py:286-303 over
+ * every chromosome, hic3defdr_amd.parallel.bh_sharded; the rank exchange is
+ * the caller's). Device buffers on the ctx stream, each call returns once
+ * the stream has drained (the caller moves the results between ranks next);
+ * every q has h3d_bh_dev's bits.
+ *   _sort: (p, val) pairs sorted by p ascending, non-finite p last (key
+ *     +inf); val NULL = 0..n-1; *m_finite (host, synchronous) = finite count.
+ *   _scan: for a bucket of mb sorted finite p-values at global ranks
+ *     offset .. offset + mb - 1 of m: scanned[j] = min over j' >= j of
+ *     p[j'] / ((offset + j' + 1) / m); *bucket_min (host, synchronous) =
+ *     scanned[0] (+inf for an empty bucket).
+ *   _finish: q[j] = min(scanned[j], higher_min) clipped at 1, higher_min =
+ *     the minimum of the higher buckets' bucket_min (+inf for the last). */
+int h3d_bh_sort_dev(h3d_ctx* ctx, const double* d_p, const int64_t* d_val, int64_t n,
+                    double* d_key_out, int64_t* d_val_out, int64_t* m_finite);
+int h3d_bh_scan_dev(h3d_ctx* ctx, const double* d_ps, int64_t mb, int64_t offset,
+                    int64_t m, double* d_scanned, double* bucket_min);
+int h3d_bh_finish_dev(h3d_ctx* ctx, const double* d_scanned, int64_t mb, double higher_min,
+                      double* d_q);
 
 /* ---- threshold / classify / collect (host) ------------------------------ */
 

@@ -305,3 +305,72 @@ def test_genome_partition_world3_equals_single_process():
     for o in outs:
         np.testing.assert_array_equal(o['q'], allq[off:off + len(o['p'])])
         off += len(o['p'])
+
+
+class _HostBhOps(object):
+    """bh_sharded's per-rank pieces in numpy (the CPU stand-in for
+    parallel.DeviceBhOps): the same sort / ratio / reverse-minimum
+    arithmetic as h3d_bh_sort_dev / _scan_dev / _finish_dev."""
+
+    def sort(self, keys, vals=None):
+        import torch
+        k = keys.numpy()
+        key = np.where(np.isfinite(k), k, np.inf)
+        o = np.argsort(key, kind='stable')
+        v = np.arange(len(k)) if vals is None else vals.numpy()
+        return (torch.from_numpy(key[o]), torch.from_numpy(v[o].astype(np.int64)),
+                int(np.isfinite(k).sum()))
+
+    def scan(self, ps, offset, m):
+        import torch
+        p = ps.numpy()
+        j = np.arange(len(p), dtype=np.float64)
+        ratio = p / ((offset + j + 1) / float(m))
+        sc = np.minimum.accumulate(ratio[::-1])[::-1].copy()
+        return torch.from_numpy(sc), (float(sc[0]) if len(sc) else np.inf)
+
+    def finish(self, scanned, higher_min):
+        import torch
+        return torch.from_numpy(np.minimum(np.minimum(scanned.numpy(),
+                                                      higher_min), 1.0))
+
+
+def _bh_sharded_worker(rank, world, port, parts, result_file):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    q = parallel.bh_sharded(torch.from_numpy(parts[rank]), _HostBhOps(),
+                            samples=8)
+    np.save(result_file % rank, q.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_bh_sharded_equals_single_process(world):
+    """parallel.bh_sharded (splitters from count-weighted samples, the
+    all_to_all by value range, the bucket's global offset, the reverse
+    minimum completed across buckets, the return all_to_all) gives every
+    p-value the single-process BH's q bit for bit: ties (many across the
+    splitters), NaN and +inf p-values, an all-NaN rank and a rank with a
+    single p-value."""
+    rng = np.random.default_rng(11)
+    p = rng.uniform(0, 1, 4000) ** 4
+    p[rng.integers(0, 4000, 900)] = 1.0          # a heavy tie at the top
+    p[rng.integers(0, 4000, 300)] = 0.25          # and one in the middle
+    p[rng.integers(0, 4000, 50)] = np.nan
+    p[rng.integers(0, 4000, 5)] = np.inf
+    sizes = [2500, 1, 1499] if world == 3 else [3999, 1]
+    parts = np.split(p, np.cumsum(sizes)[:-1])
+    if world == 3:
+        parts[1] = np.array([np.nan])
+    want = oracle.adjust_pvalues(np.concatenate(parts))
+    with tempfile.TemporaryDirectory() as tmp:
+        res = os.path.join(tmp, 'q%d.npy')
+        port = 29300 + (os.getpid() % 1000) + world
+        mp.spawn(_bh_sharded_worker, args=(world, port, parts, res),
+                 nprocs=world, join=True)
+        got = np.concatenate([np.load(res % r) for r in range(world)])
+    np.testing.assert_array_equal(got, want)

@@ -85,3 +85,28 @@ def test_two_ranks_run_to_qvalues_matches_reference(name, shard):
                                               g['qvalues__%s' % c] < fdr)
     finally:
         shutil.rmtree(outdir, ignore_errors=True)
+
+
+def test_bh_sharded_gpu():
+    """parallel.bh_sharded on the GPU (DeviceBhOps) with 3 ranks on cuda:0
+    over gloo, 3 M p-values with ties, NaN and a heavy tie at 1: every q
+    equals h3d_bh_dev's on the whole vector bit for bit."""
+    env = dict(os.environ, H3D_DEVICE='0', MASTER_ADDR='127.0.0.1',
+               OMP_NUM_THREADS='1')
+    port = 29650 + os.getpid() % 1000
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', '3', '--master-addr', '127.0.0.1',
+           '--master-port', str(port),
+           os.path.join(REPO, 'tests', 'dist_bh_main.py'), '3000000']
+    with tempfile.TemporaryDirectory() as tmp:
+        log = os.path.join(tmp, 'ranks.log')
+        with open(log, 'w') as fh:
+            try:
+                rc = subprocess.run(cmd, env=env, stdout=fh,
+                                    stderr=subprocess.STDOUT,
+                                    timeout=150).returncode
+            except subprocess.TimeoutExpired:
+                rc = 'timeout'
+        text = open(log).read()
+    assert rc == 0, text[-4000:]
+    assert 'bit-identical=True' in text, text[-4000:]
