@@ -211,7 +211,9 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
 template <int M>
 void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_start,
                   int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
-                  SegState* st, const int* seg_flags, double* result, int* queue) {
+                  SegState* st, const int* seg_flags, double* result, int* queue,
+                  const int32_t* gate_meta = nullptr, int live_min = 0,
+                  const int* gang_abort = nullptr) {
   ProfScope ps(ctx, "disp_nll", 0);
   auto k = k_brent<M>;
   constexpr int kBrentBlock = brent_block<M>();
@@ -235,7 +237,7 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
   (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), lds_px ? lds_px * 8 * M : 0,
                      ctx->stream, pd, n, seg_start, S, C, rep_idx, n_rep, st, seg_flags,
-                     result, queue, ctx->work_count, lds_px);
+                     result, queue, ctx->work_count, lds_px, gate_meta, live_min, gang_abort);
 }
 
 // the gang variant (k_brent_gang): every live segment's search over the
@@ -250,6 +252,28 @@ struct GangTables {
   int* abort = nullptr;
   long long timeout = 0;
 };
+
+// next tag epoch of the gang exchange: the tags are cleared only when their
+// buffer is new or the epoch wraps (tag = epoch << 10 | evaluation + 1)
+int gang_next_epoch(h3d_ctx* ctx, const GangTables& g, int S) {
+  if (ctx->gang_tag_buf != (void*)g.tag || ctx->gang_epoch >= (1 << 20)) {
+    if (hipMemsetAsync(g.tag, 0, (size_t)2 * S * g.gmax * 4, ctx->stream) != hipSuccess)
+      return -1;
+    ctx->gang_tag_buf = (void*)g.tag;
+    ctx->gang_epoch = 0;
+  }
+  return ++ctx->gang_epoch;
+}
+
+// spin bound of a gang wait: 0.5 s of the constant-rate wall clock
+long long gang_timeout(h3d_ctx* ctx) {
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) !=
+          hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  return (long long)khz * 500;
+}
 
 // Returns 1 (nothing set up) when one workgroup per segment already fills
 // the chip -- the gang's exchange only pays where CUs would idle -- or when
@@ -313,13 +337,44 @@ int gang_setup(h3d_ctx* ctx, const std::vector<int64_t>& seg_start, int D, int C
   HIP_TRY(hipMemsetAsync(g->abort, 0, 4, ctx->stream));
   // the host vectors die here: the copies must have read them
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  // spin bound: 0.5 s of the constant-rate wall clock
-  int khz = 0;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) !=
-          hipSuccess ||
-      khz <= 0)
-    khz = 100000;
-  g->timeout = (long long)khz * 500;
+  g->timeout = gang_timeout(ctx);
+  return 0;
+}
+
+// Device-built gang tables (the dev_tables path, no host sync): the slice
+// size from the call's pixel count alone -- about two resident grids of
+// slices over all segments, at least 1024 pixels, and few enough slices per
+// segment to be co-resident (G <= grid) --, room for the task table
+// (k_disp_tables fills it) and the exchange buffers sized for the largest
+// possible segment (all n pixels).
+template <int M>
+int gang_setup_dev(h3d_ctx* ctx, int64_t n, int D, int C, GangTables* g) {
+  auto k = k_brent_gang<M>;
+  int& nb = ctx->resident[(const void*)k];
+  if (nb == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kGangThreads, 0) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+  }
+  g->grid = ctx->n_cu * nb;
+  const int64_t total = n * C;
+  int64_t P = (total + 2 * (int64_t)g->grid - 1) / (2 * (int64_t)g->grid);
+  P = std::max<int64_t>(P, (n + g->grid - 1) / g->grid);
+  P = std::max<int64_t>(1024, (P + kGangThreads - 1) / kGangThreads * kGangThreads);
+  g->P = P;
+  g->gmax = (int)std::max<int64_t>(1, (n + P - 1) / P);
+  g->T = (int)std::min<int64_t>(INT32_MAX, (int64_t)C * (g->gmax + D));
+  const int S = D * C;
+  g->task_seg = (int32_t*)scratch(ctx, "gang_seg", (size_t)g->T * 4);
+  g->task_g = (int32_t*)scratch(ctx, "gang_g", (size_t)g->T * 4);
+  g->part = (double*)scratch(ctx, "gang_part", (size_t)2 * S * g->gmax * 8);
+  g->tag = (int*)scratch(ctx, "gang_tag", (size_t)2 * S * g->gmax * 4);
+  g->abort = (int*)scratch(ctx, "gang_abort", 4);
+  if (!g->task_seg || !g->task_g || !g->part || !g->tag || !g->abort)
+    return fail(H3D_ENOMEM, "gang tables");
+  HIP_TRY(hipMemsetAsync(g->task_seg, 0xff, (size_t)g->T * 4, ctx->stream));
+  HIP_TRY(hipMemsetAsync(g->abort, 0, 4, ctx->stream));
+  g->timeout = gang_timeout(ctx);
   return 0;
 }
 
@@ -327,15 +382,16 @@ template <int M>
 void launch_brent_gang(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_start,
                        int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
                        SegState* st, const int* seg_flags, double* result, int* queue,
-                       const GangTables& g) {
+                       const GangTables& g, const int32_t* gate_meta = nullptr,
+                       int live_max = 0) {
   ProfScope ps(ctx, "disp_nll", 0);
   (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
-  (void)hipMemsetAsync(g.tag, 0, (size_t)2 * S * g.gmax * 4, ctx->stream);
+  const int epoch = gang_next_epoch(ctx, g, S);
   const int grid = std::max(1, std::min(g.T, g.grid));
   hipLaunchKernelGGL(k_brent_gang<M>, dim3(grid), dim3(kGangThreads), 0, ctx->stream, pd,
                      n, seg_start, S, C, rep_idx, n_rep, st, seg_flags, result, queue,
                      g.task_seg, g.task_g, g.T, g.P, g.part, g.tag, g.gmax, g.abort,
-                     g.timeout, ctx->work_count);
+                     g.timeout, ctx->work_count, epoch, gate_meta, live_max);
 }
 
 // algorithmic HBM bytes of the disp_work launches so far: an equalize
@@ -426,6 +482,7 @@ void h3d_close(h3d_ctx* ctx) {
   if (ctx->work_count) (void)hipFree(ctx->work_count);
   if (ctx->h_meta) (void)hipHostFree(ctx->h_meta);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_stage_done) (void)hipEventDestroy(ctx->h_stage_done);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
@@ -481,6 +538,14 @@ int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
 // ---------------------------------------------------------------------------
 
 namespace {
+// H3D_DEBUG: the first launch error of the estimate_disp driver, by site
+void dbg_launch(const char* where) {
+  static const bool on = std::getenv("H3D_DEBUG") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "[h3d] launch error at %s: %s\n", where, hipGetErrorString(e));
+}
+
 // h3d_estimate_disp_dev's request: the smoothed tables of the result, on the
 // device, enqueued behind the result copies
 struct TableReq {
@@ -532,6 +597,11 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   std::vector<int32_t> rep_idx;
   if (int rc = check_cond(cond_of_rep, R, C, &nrep, &rep_idx)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
+  if (std::getenv("H3D_DEBUG")) {
+    const hipError_t pe = hipGetLastError();
+    if (pe != hipSuccess)
+      fprintf(stderr, "[h3d] estimate_disp entry: pending HIP error %s\n", hipGetErrorString(pe));
+  }
   hipStream_t s = ctx->stream;
   const int S = D * C;
   const int maxnr = *std::max_element(nrep.begin(), nrep.end());
@@ -801,10 +871,36 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));
   int* d_bad = (int*)scratch(ctx, "dist_bad", 4);
   if (!d_bad) return fail(H3D_ENOMEM, "dist_bad");
+  // (an M = 6 instantiation for cfg4's R_c = 6 measured equal to M = 8:
+  // 111.5 vs 110.5 ms equalize per step, profiles/r02/q2)
+  const int mslot = (maxnr <= 2 && ctx->disp_m2) ? 2
+                    : maxnr <= 4                  ? 4
+                    : maxnr <= 8                  ? 8
+                    : maxnr <= 16                 ? 16
+                                                  : 32;
+  // dev_tables, single rank: k_brent and k_brent_gang are both launched every
+  // qcml iteration and the DEVICE picks one by the live-segment count (one
+  // workgroup per segment while they fill the CUs, gangs for the tail
+  // iterations, whose few live segments left most CUs idle: cfg2's fourth
+  // iteration ran ~55 searches on 55 CUs for 0.36 ms); the gang task table
+  // comes from k_disp_tables
+  GangTables gang;
+  const bool dual = dev_tables && !reduce && ctx->brent_gang == 1;
+  if (dual) {
+    const int grc = mslot == 2    ? gang_setup_dev<2>(ctx, n, D, C, &gang)
+                    : mslot == 4  ? gang_setup_dev<4>(ctx, n, D, C, &gang)
+                    : mslot == 8  ? gang_setup_dev<8>(ctx, n, D, C, &gang)
+                    : mslot == 16 ? gang_setup_dev<16>(ctx, n, D, C, &gang)
+                                  : gang_setup_dev<32>(ctx, n, D, C, &gang);
+    if (grc) return grc;
+  }
   if (dev_tables) {
     const int64_t* d_seg0 = (const int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
     hipLaunchKernelGGL(k_disp_tables, dim3(1), dim3(1024), 0, s, d_seg0, D, C, n, d_nrep,
-                       d_cs, d_cl, d_cd, d_scb, d_sce, d_st, d_lpx, d_bad);
+                       d_cs, d_cl, d_cd, d_scb, d_sce, d_st, d_lpx, d_bad,
+                       dual ? gang.P : (int64_t)1, dual ? gang.task_seg : nullptr,
+                       dual ? gang.task_g : nullptr);
+    dbg_launch("k_disp_tables");
   }
   stamp("tables uploaded");
 
@@ -814,13 +910,19 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                      d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
   if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 32, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
-  // (an M = 6 instantiation for cfg4's R_c = 6 measured equal to M = 8:
-  // 111.5 vs 110.5 ms equalize per step, profiles/r02/q2)
-  const int mslot = (maxnr <= 2 && ctx->disp_m2) ? 2
-                    : maxnr <= 4                  ? 4
-                    : maxnr <= 8                  ? 8
-                    : maxnr <= 16                 ? 16
-                                                  : 32;
+  const size_t res_bytes = (size_t)S * 8 + (size_t)S * sizeof(SegState) + 8;
+  if (ctx->h_res_bytes < res_bytes) {
+    if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+    ctx->h_res = nullptr;
+    ctx->h_res_bytes = 0;
+    HIP_TRY(hipHostMalloc(&ctx->h_res, res_bytes, hipHostMallocDefault));
+    ctx->h_res_bytes = res_bytes;
+  }
+  double* h_resd = (double*)ctx->h_res;
+  SegState* h_sst = (SegState*)(h_resd + S);
+  int* h_bad = (int*)(h_sst + S);
+  *h_bad = 0;
+  bool have_res = false;  // the results of the final poll are in h_res
   int rounds = 0, batch = 2, rc = 0;
   if (!reduce) {
     // Single rank: one equalize pass per qcml iteration over every segment
@@ -835,8 +937,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     // H3D_BRENT: 1 (default) = gang searches (k_brent_gang) when the
     // segments are fewer than the CUs, 2 = always, 0 = one workgroup per
     // segment (k_brent)
-    GangTables gang;
     bool use_gang = ctx->brent_gang != 0 && n > 0 && !dev_tables;
+    bool dual_on = dual;
     if (use_gang) {
       int grc = mslot == 2   ? gang_setup<2>(ctx, seg_start, D, C, &gang)
                 : mslot == 4 ? gang_setup<4>(ctx, seg_start, D, C, &gang)
@@ -855,11 +957,20 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 #define H3D_QCML_ITER(MM)                                                                 \
   launch_disp_work<MM, false>(ctx, max_items, raw_s, f_s, pd, n, d_cs, d_cl, d_cd, C,     \
                               d_repidx, d_nrep, d_st, d_flags, d_list, d_meta, d_partial); \
-  if (use_gang)                                                                           \
+  dbg_launch("equalize");                                                                 \
+  if (dual_on) {                                                                          \
+    launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res,      \
+                     d_queue, d_meta, ctx->n_cu, gang.abort);                              \
+    dbg_launch("k_brent (dual)");                                                         \
+    launch_brent_gang<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, \
+                          d_queue, gang, d_meta, ctx->n_cu);                              \
+    dbg_launch("k_brent_gang (dual)");                                                    \
+  } else if (use_gang)                                                                    \
     launch_brent_gang<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, \
                           d_queue, gang);                                                 \
   else                                                                                    \
     launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
+        dbg_launch("before qcml iteration");
         if (mslot == 2) { H3D_QCML_ITER(2); }
         else if (mslot == 4) { H3D_QCML_ITER(4); }
         else if (mslot == 8) { H3D_QCML_ITER(8); }
@@ -874,17 +985,51 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         }
         ++rounds;
       }
+      // the poll, and speculatively what follows a final one: the result
+      // copies (pinned) and the requested smoother behind them, so a final
+      // poll costs one host round trip (r03s trace: ~0.12 ms of host gaps
+      // after the fifth iteration); a poll that finds live segments simply
+      // runs them, and a later poll redoes both
+      hipEvent_t copied = ev_get(ctx);
       if (hipMemcpyAsync(h_meta, d_meta, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
-          (use_gang &&
+          ((use_gang || dual_on) &&
            hipMemcpyAsync(h_meta + 4, gang.abort, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-          hipStreamSynchronize(s) != hipSuccess) {
-        rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(hipGetLastError()));
+          hipMemcpyAsync(h_resd, d_res, (size_t)S * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipMemcpyAsync(h_sst, d_st, (size_t)S * sizeof(SegState), hipMemcpyDeviceToHost, s) !=
+              hipSuccess ||
+          (dev_tables && hipMemcpyAsync(h_bad, d_bad, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+          hipEventRecord(copied, s) != hipSuccess) {
+        ctx->event_pool.push_back(copied);
+        rc = fail(H3D_EHIP, "disp round copies failed: %s", hipGetErrorString(hipGetLastError()));
         break;
       }
+      if (treq) {
+        rc = h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac, treq->aff,
+                                 treq->d_tables);
+        if (rc) {
+          (void)hipEventSynchronize(copied);
+          ctx->event_pool.push_back(copied);
+          break;
+        }
+      }
+      const hipError_t ce = hipEventSynchronize(copied);
+      ctx->event_pool.push_back(copied);
+      if (ce != hipSuccess) {
+        rc = fail(H3D_EHIP, "disp round sync failed: %s", hipGetErrorString(ce));
+        break;
+      }
+      have_res = true;
       stamp("poll");
       if (std::getenv("H3D_DEBUG"))
         fprintf(stderr, "[h3d] qcml iterations=%d live_segments=%d gang=%d abort=%d\n",
-                rounds, h_meta[3], (int)use_gang, use_gang ? h_meta[4] : 0);
+                rounds, h_meta[3], use_gang ? 1 : dual_on ? 2 : 0,
+                (use_gang || dual_on) ? h_meta[4] : 0);
+      if (dual_on && h_meta[4]) {
+        // a gang aborted: k_brent (gated on the same flag) already took over
+        // the following iterations on the device; launch it alone from here
+        dual_on = false;
+        ctx->gang_aborts += 1;
+      }
       if (use_gang && h_meta[4]) {
         // a gang's wait timed out (CUs held elsewhere): its segments stayed
         // in kEqualize and repeat their iteration; finish with k_brent
@@ -963,25 +1108,28 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     batch = std::min(batch * 2, 8);
   }
   if (rc) return rc;
+  // a launch error of the qcml loop is this call's, not a later call's
+  HIP_TRY(hipGetLastError());
   std::vector<int32_t> fl(S);
-  int bad = 0;
-  HIP_TRY(hipMemcpyAsync(disp_per_dist, d_res, S * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(st.data(), d_st, S * sizeof(SegState), hipMemcpyDeviceToHost, s));
-  if (dev_tables) HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
-  if (treq) {
-    // the smoother runs behind the result copies; the host waits for the
-    // copies only, so the kernel overlaps the return to the caller
+  if (!have_res) {
+    // (the multi-rank path) the results into the pinned zone; the smoother
+    // runs behind the copies, the host waits for the copies only
+    HIP_TRY(hipMemcpyAsync(h_resd, d_res, (size_t)S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_sst, d_st, (size_t)S * sizeof(SegState), hipMemcpyDeviceToHost, s));
+    if (dev_tables) HIP_TRY(hipMemcpyAsync(h_bad, d_bad, 4, hipMemcpyDeviceToHost, s));
     hipEvent_t copied = ev_get(ctx);
     HIP_TRY(hipEventRecord(copied, s));
-    const int trc = h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac,
-                                        treq->aff, treq->d_tables);
+    const int trc = treq ? h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac,
+                                               treq->aff, treq->d_tables)
+                         : 0;
     const hipError_t e = hipEventSynchronize(copied);
     ctx->event_pool.push_back(copied);
     if (trc) return trc;
     if (e != hipSuccess) return fail(H3D_EHIP, "result copy: %s", hipGetErrorString(e));
-  } else {
-    HIP_TRY(hipStreamSynchronize(s));
   }
+  std::memcpy(disp_per_dist, h_resd, (size_t)S * 8);
+  std::memcpy(st.data(), h_sst, (size_t)S * sizeof(SegState));
+  const int bad = dev_tables ? *h_bad : 0;
   stamp("results");
   if (bad) return fail(H3D_EARG, "dist outside [0, %d)", D);
   int all = 0;

@@ -87,6 +87,11 @@ struct h3d_ctx {
   // pinned staging of estimate_disp's per-call tables (one H2D copy)
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
+  // pinned landing zone of estimate_disp's results (per-segment dispersion,
+  // state, the distance check): pageable device-to-host copies blocked the
+  // host one after another at the end of every call
+  void* h_res = nullptr;
+  size_t h_res_bytes = 0;
   // recorded after each H2D copy out of h_stage: the next call waits on it
   // before rewriting (or freeing) the buffer, whichever way the last call
   // returned
@@ -118,6 +123,10 @@ struct h3d_ctx {
   // h3d_set_live_hint: (distance, condition) segments with pixels in the
   // next estimate_disp call as the caller knows them (0 = unknown: all D x C)
   int64_t live_hint = 0;
+  // k_brent_gang tag epoch (tags carry it, so they need no clearing between
+  // launches) and the tag buffer it is valid for
+  int gang_epoch = 0;
+  void* gang_tag_buf = nullptr;
   h3dint::TablePending tab_pending;
   // H3D_DEV_SEG_TABLES (default 1): estimate_disp's chunk / segment tables
   // built on the device (k_disp_tables) where no gangs are needed

@@ -251,18 +251,23 @@ static __global__ void k_seg_bounds(const int32_t* __restrict__ dist_s, int64_t 
 // (chunk_start / len / distance, scanned over the distances in order), the
 // first / end chunk of each distance, every segment's initial qcml state and
 // pixel count. One 1024-thread block. *bad = 1 when a pixel's distance is
-// outside [0, D) (seg_start does not span [0, n)).
+// outside [0, D) (seg_start does not span [0, n)). With task_seg non-null
+// also k_brent_gang's task table: per distance C x ceil(len / gang_P)
+// (segment, slice) entries in distance order (the caller pre-fills the
+// table's unused tail with -1).
 static __global__ __launch_bounds__(1024) void k_disp_tables(
     const int64_t* __restrict__ seg, int D, int C, int64_t n,
     const int32_t* __restrict__ n_rep, int64_t* __restrict__ cs,
     int32_t* __restrict__ cl, int32_t* __restrict__ cd, int32_t* __restrict__ scb,
     int32_t* __restrict__ sce, SegState* __restrict__ st, int64_t* __restrict__ lpx,
-    int* __restrict__ bad) {
-  __shared__ int s_wsum[16];
-  __shared__ int s_carry;
+    int* __restrict__ bad, int64_t gang_P, int32_t* __restrict__ task_seg,
+    int32_t* __restrict__ task_g) {
+  __shared__ int s_wsum[16], s_tsum[16];
+  __shared__ int s_carry, s_tcarry;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     s_carry = 0;
+    s_tcarry = 0;
     *bad = (seg[0] != 0 || seg[D] != n) ? 1 : 0;
   }
   __syncthreads();
@@ -270,20 +275,38 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
     const int d = base + threadIdx.x;
     const int64_t len = d < D ? seg[d + 1] - seg[d] : 0;
     const int nch = (int)((len + kChunk - 1) / kChunk);
-    int x = nch;  // inclusive scan over the block
+    // gang tasks of the distance (k_brent_gang): C x ceil(len / P) slices
+    const int ntk = task_seg ? C * (int)((len + gang_P - 1) / gang_P) : 0;
+    int x = nch, xt = ntk;  // inclusive scans over the block
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
+      const int y = __shfl_up(x, off, 64), yt = __shfl_up(xt, off, 64);
+      if (lane >= off) {
+        x += y;
+        xt += yt;
+      }
     }
-    if (lane == 63) s_wsum[wid] = x;
+    if (lane == 63) {
+      s_wsum[wid] = x;
+      s_tsum[wid] = xt;
+    }
     __syncthreads();
-    int before = 0, tot = 0;
+    int before = 0, tot = 0, tbefore = 0, ttot = 0;
     for (int w = 0; w < 16; ++w) {
       before += (w < wid) ? s_wsum[w] : 0;
       tot += s_wsum[w];
+      tbefore += (w < wid) ? s_tsum[w] : 0;
+      ttot += s_tsum[w];
     }
     const int b0 = s_carry + before + x - nch;
+    if (d < D && ntk) {
+      const int t0 = s_tcarry + tbefore + xt - ntk, G = ntk / C;
+      for (int c = 0; c < C; ++c)
+        for (int j = 0; j < G; ++j) {
+          task_seg[t0 + c * G + j] = d * C + c;
+          task_g[t0 + c * G + j] = j;
+        }
+    }
     if (d < D) {
       scb[d] = b0;
       sce[d] = b0 + nch;
@@ -299,7 +322,10 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
+    if (threadIdx.x == 0) {
+      s_carry += tot;
+      s_tcarry += ttot;
+    }
     __syncthreads();
   }
 }
@@ -673,8 +699,13 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     const int32_t* __restrict__ n_rep /* C */, SegState* __restrict__ st,
     const int* __restrict__ seg_flags, double* __restrict__ result,
     int* __restrict__ queue, unsigned long long* __restrict__ work_count,
-    int64_t lds_px) {
+    int64_t lds_px, const int32_t* __restrict__ gate_meta, int live_min,
+    const int* __restrict__ gang_abort) {
   extern __shared__ double s_pd[];  // [nr][lds_px]
+  // gate (device-side choice between this kernel and k_brent_gang, both
+  // launched): run when the live segments fill the chip, or when a gang
+  // has aborted
+  if (gate_meta && gate_meta[3] < live_min && !(gang_abort && *gang_abort)) return;
   // the state machine lives in LDS and is stepped by thread 0; the data loop
   // only holds the four NLL constants (the SegState in every thread's VGPRs
   // spilled at the 1024-thread register budget)
@@ -818,9 +849,13 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
     const int* __restrict__ seg_flags, double* __restrict__ result,
     int* __restrict__ queue, const int32_t* __restrict__ task_seg,
     const int32_t* __restrict__ task_g, int T, int64_t P,
-    double* __restrict__ part /* 2 x S x gmax */, int* __restrict__ tag /* 2 x S x gmax, zeroed */,
+    double* __restrict__ part /* 2 x S x gmax */, int* __restrict__ tag /* 2 x S x gmax */,
     int gmax, int* __restrict__ abort_flag, long long timeout,
-    unsigned long long* __restrict__ work_count) {
+    unsigned long long* __restrict__ work_count, int epoch,
+    const int32_t* __restrict__ gate_meta, int live_max) {
+  // gate (device-side choice, see k_brent): run while the live segments
+  // leave CUs idle, unless a gang has aborted
+  if (gate_meta && (gate_meta[3] >= live_max || *abort_flag)) return;
   __shared__ SegState s_st;
   __shared__ double wpart[kGangThreads / 64];
   __shared__ int s_next, s_more, s_abort;
@@ -832,6 +867,7 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
     const int t = s_next;
     if (t >= T) break;
     const int s = task_seg[t], g = task_g[t];
+    if (s < 0) continue;  // unused entry of a device-built task table
     // every member reads the phase before the gang's first evaluation, so
     // before member 0 can write the segment back
     if (st[s].phase != kEqualize) continue;
@@ -884,7 +920,10 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
         bool ok = true;
         if (G > 1) {
           const size_t base = ((size_t)(evals & 1) * S + s) * gmax;
-          const int want = evals + 1;
+          // tags carry the launch's epoch: no tag from an earlier launch
+          // matches, so the tags need no clearing between launches
+          // (evals < kMaxFun = 500 < 1024)
+          const int want = (epoch << 10) | (evals + 1);
           if (lane == 0) {
             __hip_atomic_store(&part[base + g], mine, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

@@ -52,6 +52,11 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   std::vector<int32_t> rep_idx;
   if (int rc = check_cond(cond_of_rep, R, C, &nrep, &rep_idx)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
+  if (getenv("H3D_DEBUG")) {
+    const hipError_t pe = hipGetLastError();
+    if (pe != hipSuccess)
+      fprintf(stderr, "[h3d] lrt entry: pending HIP error %s\n", hipGetErrorString(pe));
+  }
   hipStream_t s = ctx->stream;
   // d_dist == NULL: disp_table holds per-pixel dispersions (n, C), or with
   // `wide` per pixel and replicate (n, R)

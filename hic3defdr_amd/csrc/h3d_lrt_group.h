@@ -232,14 +232,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
         if (c == cnd[s]) m1k = m1[c];
       const double xk = (double)x[s];
       const double r = 1.0 / a[s];
-      // the prefix is common to the null and alt rows and cancels in llr up
-      // to their rounding: the branch-light lgam_nll, as k_lrt
-      const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) +
-                         r * log(r);
+      // the mean-free prefix of logpmf is common to the null and alt rows
+      // and cancels in llr: left out, as k_lrt (lrt_pixel)
       const double m0k = m0 * fv[s], m1f = m1k * fv[s];
       const double l0 = log(r + m0k), l1 = log(r + m1f);
-      tn[s] = pre - r * l0 + xk * log(m0k) - xk * l0;
-      ta[s] = pre - r * l1 + xk * log(m1f) - xk * l1;
+      tn[s] = -r * l0 + xk * log(m0k) - xk * l0;
+      ta[s] = -r * l1 + xk * log(m1f) - xk * l1;
     }
     const double lv = np_sum_g8<J>(tn, R, lane, base) - np_sum_g8<J>(ta, R, lane, base);
     fl_all |= st;

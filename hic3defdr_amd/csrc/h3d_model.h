@@ -412,22 +412,19 @@ H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
 #pragma unroll
       for (int c = 0; c < CM; ++c)
         if (c == cond[k]) m1 = mu1[c];
-      // logpmf (scaled_nb.py:31-33) under the null and the alt mean: Python
-      // evaluates it left to right, so the terms without m form one common
-      // prefix, computed once (3 of the 6 lgammas and r log r). The prefix
-      // enters the null and the alt row alike and cancels in llr up to the
-      // rows' rounding, so its lgammas take the NLL's lgam_nll (absolute
-      // error ~1e-15, no data-dependent loop or division) instead of cephes
-      // lgam: k_lrt<4,2> 0.86 -> 0.75 ms per cfg2 step, llr unchanged at the
-      // tests' 1e-10 absolute bar
+      // logpmf (scaled_nb.py:31-33) under the null and the alt mean. The
+      // terms without m -- gammaln(r + k) - gammaln(k + 1) - gammaln(r) +
+      // r log r, Python's left-to-right prefix -- are the same in the null
+      // and the alt row of a replicate and cancel in llr = sum(null) -
+      // sum(alt) exactly; only the rows' rounding sees them (the reference's
+      // rows carry ~ulp(gammaln(r + k)) of it). They are left out: llr moves
+      // by that rounding only (12 lgammas + 4 logs per pixel fewer)
       const double xk = (double)x[k];
       const double r = 1.0 / a[k];
-      const double pre = lgam_nll(r + xk) - lgam_nll(xk + 1) - lgam_nll(r) +
-                         r * log_fast_checked(r);
       const double m0k = *mu0 * f[k], m1k = m1 * f[k];
       const double l0 = log_fast_checked(r + m0k), l1 = log_fast_checked(r + m1k);
-      tn.add(k, pre - r * l0 + xk * log_fast_checked(m0k) - xk * l0);
-      ta.add(k, pre - r * l1 + xk * log_fast_checked(m1k) - xk * l1);
+      tn.add(k, -r * l0 + xk * log_fast_checked(m0k) - xk * l0);
+      ta.add(k, -r * l1 + xk * log_fast_checked(m1k) - xk * l1);
     }
   }
   *llr = tn.sum() - ta.sum();

@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--bins', type=int, default=1500)
     ap.add_argument('--dmax', type=int, default=250)
+    ap.add_argument('--key', choices=('maxmin', 'minmax', 'summax', 'summin', 'total'), default='maxmin')
     args = ap.parse_args()
     import oracle
     from hic3defdr_amd import synthetic
@@ -56,14 +57,31 @@ def main():
     dist = col - row
     _, dpd, _ = oracle.estimate_disp([prep], [bias], design,
                                      dist_thresh_max=args.dmax)
-    order = np.lexsort((raw.sum(1), dist))
-    raw, f, dist = raw[order], np.ascontiguousarray(f[order]), dist[order]
-    n, R = raw.shape
     cond = design.argmax(axis=1)
+    raw0, f0, dist0 = raw, f, dist
     P = ctypes.c_void_p
     lib.q2qs_equalize.argtypes = [ctypes.c_int64, ctypes.c_int, P, P, P,
                                   ctypes.c_int, P, P, P]
     for c in range(design.shape[1]):
+        # the kernel's pixel order: per condition (distance, max, min count
+        # of the condition's replicates, each capped to 12 bits)
+        # (k_dist_cond_keys); --key total: (distance, all replicates' total)
+        rc = raw0[:, cond == c]
+        mx, mn = np.minimum(rc.max(1), 4095), np.minimum(rc.min(1), 4095)
+        sm = np.minimum(rc.sum(1), 4095)
+        if args.key == 'total':
+            order = np.lexsort((raw0.sum(1), dist0))
+        elif args.key == 'minmax':
+            order = np.lexsort((mx, mn, dist0))
+        elif args.key == 'summax':
+            order = np.lexsort((mx, sm, dist0))
+        elif args.key == 'summin':
+            order = np.lexsort((mn, sm, dist0))
+        else:
+            order = np.lexsort((mn, mx, dist0))
+        raw, f, dist = raw0[order], np.ascontiguousarray(f0[order]), \
+            dist0[order]
+        n, R = raw.shape
         reps = np.flatnonzero(cond == c).astype(np.int32)
         nr = len(reps)
         alpha = np.ascontiguousarray(dpd[dist, c])
