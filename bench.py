@@ -615,10 +615,8 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
     if emu:
         own = [p for i, p in enumerate(parts) if i in mine]
         d_all = np.concatenate([p[2] for p in parts])
-        d_cnt = np.bincount(d_all, minlength=D)[:D]
-        owner = parallel.distance_owners(d_cnt, e_world)
-        # the rank's live segments, as disp_per_dist_by_distance hints them
-        e_live = int(((owner == e_rank) & (d_cnt > 0)).sum()) * 2
+        owner = parallel.distance_owners(
+            np.bincount(d_all, minlength=D)[:D], e_world)
         keep = owner[d_all] == e_rank
         e_raw = np.concatenate([p[0] for p in parts])[keep]
         e_f = np.concatenate([p[1] for p in parts])[keep]
@@ -654,7 +652,6 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
             dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
                                                      cond, C, D)
         elif emu:
-            ctx.set_live_hint(e_live)
             dpd = ctx.disp_per_dist_dev(te_raw.data_ptr(), te_f.data_ptr(),
                                         te_dist.data_ptr(), e_n, R, cond, C, D)
             # the other ranks' rows (not run here): interpolated over this

@@ -32,7 +32,7 @@ EXPORTS = [
     'h3d_bh_ctx', 'h3d_bh_dev', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
     'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
     'h3d_estimate_disp_dev', 'h3d_bh_sort_dev', 'h3d_bh_scan_dev',
-    'h3d_bh_finish_dev', 'h3d_set_live_hint',
+    'h3d_bh_finish_dev',
 ]
 
 
@@ -106,7 +106,6 @@ def load_library(path=None):
             'h3d_bh_sort_dev': (_I, [_P, _P, _P, _I64, _P, _P, _P]),
             'h3d_bh_scan_dev': (_I, [_P, _P, _I64, _I64, _I64, _P, _P]),
             'h3d_bh_finish_dev': (_I, [_P, _P, _I64, _D, _P]),
-            'h3d_set_live_hint': (_I, [_P, _I64]),
             'h3d_profile_enable': (_I, [_P, _I]),
             'h3d_profile_read': (_I, [_P, ctypes.c_char_p, _P, _P, _P]),
             'h3d_profile_reset': (_I, [_P]),
@@ -388,11 +387,6 @@ class Context(object):
     def bh_dev(self, d_p, n, d_q):
         _check(self.lib.h3d_bh_dev(self.handle, _P(d_p), n, _P(d_q)),
                'h3d_bh_dev')
-
-    def set_live_hint(self, live_segments):
-        """Segments with pixels in the next estimate_disp call (h3d.h)."""
-        _check(self.lib.h3d_set_live_hint(self.handle, int(live_segments)),
-               'h3d_set_live_hint')
 
     # pieces of the rank-sharded BH (parallel.bh_sharded, h3d.h)
     def bh_sort_dev(self, d_p, d_val, n, d_key_out, d_val_out):

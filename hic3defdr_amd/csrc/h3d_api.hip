@@ -494,13 +494,6 @@ int h3d_set_stream(h3d_ctx* ctx, void* stream) {
   return 0;
 }
 
-int h3d_set_live_hint(h3d_ctx* ctx, int64_t live_segments) {
-  if (!ctx) return fail(H3D_EARG, "null ctx");
-  if (live_segments < 0) return fail(H3D_EARG, "negative live segment count");
-  ctx->live_hint = live_segments;
-  return 0;
-}
-
 int h3d_profile_enable(h3d_ctx* ctx, int on) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   prof_collect(ctx);
@@ -610,14 +603,12 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   // before the qcml loop -- single rank, and enough segments that the Brent
   // searches need no gangs (whose task tables the host builds from the
   // segment bounds)
-  // (a rank of the distance re-shard holds pixels of ~D / world distances:
-  // its caller's live-segment hint keeps gangs there; r03u measured the
-  // N = 8 cfg3 rank without it: Brent 25.9 vs 5.1 ms per step)
-  const int64_t live = ctx->live_hint > 0 ? std::min<int64_t>(S, ctx->live_hint) : S;
-  ctx->live_hint = 0;
-  const bool dev_tables = ctx->dev_seg_tables && !reduce && n > 0 &&
-                          ctx->brent_gang != 2 &&
-                          (live >= ctx->n_cu || ctx->brent_gang == 0);
+  // (any number of live segments: the Brent mode -- one workgroup per
+  // segment or gangs -- is chosen on the device per qcml iteration, so a rank
+  // of the distance re-shard, whose ~D / world live segments leave CUs idle,
+  // needs no host-built gang tables either; r03z: its N = 8 cfg3 share 13.9
+  // ms per step with the host tables, 13.9 with these)
+  const bool dev_tables = ctx->dev_seg_tables && !reduce && n > 0 && ctx->brent_gang != 2;
 
   // 1. stable sort of the pixels by distance, SoA gather
   std::vector<int64_t> seg_start(D + 1, 0);

@@ -120,9 +120,6 @@ struct h3d_ctx {
   // H3D_BRENT_LDS_KB: LDS per k_brent workgroup for the segment's staged
   // head (0 = stream every evaluation from memory)
   int brent_lds_kb = 144;
-  // h3d_set_live_hint: (distance, condition) segments with pixels in the
-  // next estimate_disp call as the caller knows them (0 = unknown: all D x C)
-  int64_t live_hint = 0;
   // k_brent_gang tag epoch (tags carry it, so they need no clearing between
   // launches) and the tag buffer it is valid for
   int gang_epoch = 0;

@@ -144,11 +144,6 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
         raw_m = torch.empty((0, R), dtype=torch.int32, device=dev)
         f_m = torch.empty((0, R), dtype=torch.float64, device=dev)
         dist_m = torch.empty(0, dtype=torch.int32, device=dev)
-    # this rank's live segments (its owned distances with pixels): with fewer
-    # than the CUs the driver splits each Brent search over a gang
-    if hasattr(ctx, 'set_live_hint'):
-        own = (owner_of == rank) & (cnt.cpu().numpy() > 0)
-        ctx.set_live_hint(max(1, int(own.sum()) * C))
     tab = ctx.disp_per_dist_dev(raw_m.data_ptr(), f_m.data_ptr(),
                                 dist_m.data_ptr(), m, R, cond_of_rep, C, D)
     tab[owner_of != rank] = 0.0

@@ -86,16 +86,6 @@ void h3d_close(h3d_ctx* ctx);
 const char* h3d_last_error(void);
 /* stream the ctx launches on (hipStream_t); NULL = the ctx's own stream */
 int h3d_set_stream(h3d_ctx* ctx, void* stream);
-/* The number of (distance, condition) segments that hold pixels in the NEXT
- * h3d_disp_per_dist[_dev] / h3d_estimate_disp_dev call, when the caller
- * knows it (0 = unknown: D x C); consumed by that call. A rank of the
- * multi-GPU distance re-shard owns ~D / world distances: with fewer live
- * segments than CUs the driver runs each Brent search over several
- * workgroups (gangs), which needs the segment bounds on the host, instead of
- * building its tables on the device without a host sync. Multi-GPU
- * addition, no reference counterpart (analysis.py:169-206 pools every
- * distance in one process). */
-int h3d_set_live_hint(h3d_ctx* ctx, int64_t live_segments);
 
 /* ---- prepare_data ------------------------------------------------------ */
 
