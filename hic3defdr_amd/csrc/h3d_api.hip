@@ -639,7 +639,10 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       HIP_TRY(hipMemcpyAsync(d_reps, rep_idx.data(), (size_t)C * kMaxReps * 4,
                              hipMemcpyHostToDevice, s));
       const bool k32 = end_bit <= 16;
-      const int cbits = k32 ? 32 - end_bit : 64 - end_bit;
+      // 32-bit keys: (distance, 8-bit min / max count codes), sorted over
+      // end_bit + 16 bits (cfg2: 24 bits, three radix passes)
+      const int cbits = k32 ? 16 : 64 - end_bit;
+      const int sort_bits = k32 ? end_bit + 16 : 64;
       void* keys = scratch(ctx, "dkeys", n * (k32 ? 4 : 8));
       void* keys_s = scratch(ctx, "dkeys_s", n * (k32 ? 4 : 8));
       if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
@@ -651,12 +654,12 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                              cbits, (uint32_t*)keys);
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)keys,
                                                      (uint32_t*)keys_s, idx_in, idx_out,
-                                                     (int)n, 0, 32, s));
+                                                     (int)n, 0, sort_bits, s));
           void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
           if (!tmp) return fail(H3D_ENOMEM, "sort temp");
           HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)keys,
                                                      (uint32_t*)keys_s, idx_in, idx_out,
-                                                     (int)n, 0, 32, s));
+                                                     (int)n, 0, sort_bits, s));
           if (c == 0)
             hipLaunchKernelGGL(k_key_dist<uint32_t>, dim3(grid_for(ctx, n)), dim3(kBlock),
                                0, s, (const uint32_t*)keys_s, n, cbits, dist_s);

@@ -171,6 +171,15 @@ static __global__ __launch_bounds__(256) void k_gather_cond_tile(
 // condition's replicates; each capped to its half of the cbits count bits).
 // Modelled on the cfg2 census (tools/order_experiment.py): wave lane
 // utilisation of the equalize pass 0.68 with the total-count key -> 0.79.
+// count code of the 16-bit key: exact below 128, then 8 counts per code up
+// to 1151 (counts that high are a few near-diagonal pixels, whose trip counts
+// vary slowly with the count): the key fits 24 bits at D <= 256, one radix
+// pass fewer than 12-bit caps (census, tools/q2q_stats.py --key: the same
+// modelled lane utilisation)
+__device__ inline uint64_t count_code8(uint64_t v) {
+  return v < 128 ? v : (v < 1152 ? 128 + ((v - 128) >> 3) : 255);
+}
+
 template <typename K>
 __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
                                  const int32_t* __restrict__ raw, int64_t n, int R,
@@ -187,10 +196,15 @@ __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
       mx = v > mx ? v : mx;
       mn = v < mn ? v : mn;
     }
-    if (mx > cap_hi) mx = cap_hi;
-    if (mn > cap_lo) mn = cap_lo;
     uint64_t d = (uint32_t)dist[i];
     if (d > dcap) d = dcap;
+    if (cbits == 16) {
+      // (distance, min code, max code): min first models 1-2 % better
+      keys[i] = (K)((d << 16) | (count_code8(mn) << 8) | count_code8(mx));
+      continue;
+    }
+    if (mx > cap_hi) mx = cap_hi;
+    if (mn > cap_lo) mn = cap_lo;
     keys[i] = (K)((d << cbits) | (mx << lo) | mn);
   }
 }

@@ -137,7 +137,8 @@ MM10_BINS = [19535, 18211, 16007, 15649, 15171, 14950, 14546, 12930, 12459,
              17102]
 
 
-def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05):
+def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05,
+              workers=8):
     """The disp pixels of one chromosome drawn directly in the distance band,
     no files (the cfg3 / cfg4 shapes, where writing NPZ files for a whole
     genome would dominate): the generator model above with unit size
@@ -145,11 +146,15 @@ def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05):
     conditions >= 1, per-bin bias exp(N(0, .25)), depth 0.8 + 0.1 (k mod 4),
     NB(1/disp) -- and disp_idx as prepare_data computes it with unit size
     factors: every condition's mean of raw / (b_i b_j) >= 1 and d >= 4.
-    The stream is seeded by (seed, chrom_index), so a rank can draw just its
-    own chromosomes and every world size sees the same genome. Returns
+    The streams are seeded by (seed, chrom_index) -- one for the band, one
+    per replicate (SeedSequence children), the replicates drawn on `workers`
+    threads (numpy's bulk draws release the GIL) -- so a rank can draw just
+    its own chromosomes and every world size sees the same genome. Returns
     (raw (n, R) int32, f (n, R) f64, dist (n,) int32)."""
-    rng = np.random.default_rng([seed, chrom_index])
+    import concurrent.futures
     R = int(sum(n_per_cond))
+    kids = np.random.SeedSequence([seed, chrom_index]).spawn(R + 1)
+    rng = np.random.default_rng(kids[0])
     cond = np.repeat(np.arange(len(n_per_cond)), n_per_cond)
     top = min(dmax, n_bins - 1)
     d = np.concatenate([np.full(n_bins - k, k, dtype=np.int32)
@@ -163,13 +168,17 @@ def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05):
     raw = np.empty((d.size, R), dtype=np.int32)
     f = np.empty((d.size, R))
     n = 1.0 / disp
-    for k in range(R):
-        b = np.exp(rng.normal(0, 0.25, n_bins))
+
+    def replicate(k):
+        g = np.random.default_rng(kids[k + 1])
+        b = np.exp(g.normal(0, 0.25, n_bins))
         bb = b[r] * b[c]
         mu = base * np.where(diff & (cond[k] >= 1), 2.0, 1.0) * bb * \
             (0.8 + 0.1 * (k % 4))
-        raw[:, k] = rng.negative_binomial(n, n / (n + mu))
+        raw[:, k] = g.negative_binomial(n, n / (n + mu))
         f[:, k] = bb
+    with concurrent.futures.ThreadPoolExecutor(max(1, min(workers, R))) as ex:
+        list(ex.map(replicate, range(R)))
     keep = d >= 4
     for ci in range(len(n_per_cond)):
         keep &= (raw[:, cond == ci] / f[:, cond == ci]).mean(axis=1) >= 1.0
@@ -187,6 +196,8 @@ def draw_genome(bins_list, n_per_cond, dmax, seed=0, indices=None,
     idx = list(range(len(bins_list))) if indices is None else list(indices)
     with concurrent.futures.ThreadPoolExecutor(max(1, min(workers,
                                                           len(idx)))) as ex:
+        # (the chromosomes in parallel, each one's replicates serially)
         return list(ex.map(lambda i: draw_band(bins_list[i], n_per_cond, dmax,
-                                               seed=seed, chrom_index=i),
+                                               seed=seed, chrom_index=i,
+                                               workers=1),
                            idx))

@@ -1,0 +1,87 @@
+"""cfg4 (BASELINE.json configs[3]) at full size: human chr1 at 5 kb --
+49,792 bins, R = 18 as three conditions of 6 replicates, dist_thresh_max
+400, ~13 M disp pixels -- through estimate_disp (the M = 8 equalize / Brent
+path, numpy's pairwise sums from 8 replicates on), the lowess tables, the
+LRT (k_lrt8<24, 4>: 8-lane groups per pixel, chi2 with 2 degrees of
+freedom) and BH on one GPU.
+
+The reference would take days on this shape (its O(fail * N) brentq
+fallback), so the whole chromosome is held to properties and a sample is
+held to the CPU restatement (oracle/, pinned to the reference's goldens at
+fixture size: r18c3, r16c2):
+- every present distance has a finite dispersion in (0, 100), absent ones
+  NaN; p in [0, 1]; positive finite means; llr <= 0 (nested models); BH =
+  the oracle's bit for bit; a second run bit-identical;
+- three whole segments (distances 4, 150, 400 in every condition): the
+  oracle's qcml on the segment's pixels (dispersion.py:10-43) vs the
+  GPU's disp_per_dist at 1e-6 (the near-tie Brent bound of
+  test_gpu_scale.py: >= 8 of the 9 at 1e-6, all within 2 xatol in delta);
+- 3,000 sampled pixels: the oracle's lrt (lrt.py:7-50) with the GPU's own
+  tables vs the GPU's p at 1e-6 relative.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BINS, NPC, DMAX = 49792, (6, 6, 6), 400
+
+
+@pytest.fixture(scope='module')
+def cfg4():
+    from hic3defdr_amd import synthetic
+    raw, f, dist = synthetic.draw_band(BINS, NPC, DMAX, seed=0)
+    cond = np.repeat(np.arange(len(NPC)), NPC).astype(np.int32)
+    return raw, f, dist, cond
+
+
+def test_cfg4_full_chromosome(cfg4):
+    import oracle
+    from hic3defdr_amd import _native
+    ctx = _native.context(0)
+    raw, f, dist, cond = cfg4
+    assert len(raw) > 10_000_000 and raw.shape[1] == 18
+    C, D = len(NPC), DMAX + 1
+    runs = []
+    for _ in range(2):
+        dpd = ctx.disp_per_dist(raw, f, dist, cond, C, D)  # raises on flags
+        tab = _native.disp_tables(dpd)
+        p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, cond, want_disp=False)
+        q = ctx.bh(p)
+        runs.append((dpd, p, llr, m0, m1, q))
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)
+    dpd, p, llr, m0, m1, q = runs[0]
+    present = np.isin(np.arange(D), dist)
+    assert present[4:].all() and not present[:4].any()
+    assert np.all(np.isfinite(dpd[present])) and np.all(np.isnan(dpd[~present]))
+    assert np.all((dpd[present] > 0) & (dpd[present] < 100.0))
+    assert np.all(np.isfinite(p)) and np.all((p >= 0) & (p <= 1))
+    assert np.all(np.isfinite(m0)) and np.all(m0 > 0)
+    assert np.all(np.isfinite(m1)) and np.all(m1 > 0)
+    assert np.all(llr <= 1e-9)
+    np.testing.assert_array_equal(q, oracle.adjust_pvalues(p))
+
+    # whole segments against the oracle's qcml
+    rel, ddelta = [], []
+    for d in (4, 150, 400):
+        sel = dist == d
+        for c in range(C):
+            reps = cond == c
+            want = oracle.qcml(raw[sel][:, reps].astype(float), f[sel][:, reps])
+            got = dpd[d, c]
+            rel.append(abs(got - want) / abs(want))
+            ddelta.append(abs(got / (1 + got) - want / (1 + want)))
+    rel, ddelta = np.array(rel), np.array(ddelta)
+    assert (rel <= 1e-6).sum() >= len(rel) - 1, rel
+    assert np.all(ddelta <= 2e-5), ddelta
+
+    # a pixel sample through the oracle's lrt with the GPU's tables
+    rng = np.random.default_rng(1)
+    idx = np.sort(rng.choice(len(raw), 3000, replace=False))
+    design = np.zeros((18, C), dtype=bool)
+    design[np.arange(18), cond] = True
+    disp = tab[dist[idx]][:, cond]          # lrt.py's per-replicate disp
+    p_o, llr_o, _, _ = oracle.lrt(raw[idx].astype(float), f[idx], disp, design)
+    np.testing.assert_allclose(p[idx], p_o, rtol=1e-6, atol=1e-300)
+    np.testing.assert_allclose(llr[idx], llr_o, rtol=1e-6, atol=1e-9)

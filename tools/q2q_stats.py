@@ -33,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--bins', type=int, default=1500)
     ap.add_argument('--dmax', type=int, default=250)
-    ap.add_argument('--key', choices=('maxmin', 'minmax', 'summax', 'summin', 'total'), default='maxmin')
+    ap.add_argument('--key', choices=('maxmin', 'maxmin8', 'minmax', 'summax', 'summin', 'total'), default='maxmin')
     args = ap.parse_args()
     import oracle
     from hic3defdr_amd import synthetic
@@ -77,6 +77,13 @@ def main():
             order = np.lexsort((mx, sm, dist0))
         elif args.key == 'summin':
             order = np.lexsort((mn, sm, dist0))
+        elif args.key == 'maxmin8':
+            # 8-bit count codes: exact below 128, then 8 counts per code up
+            # to 1151 (k_dist_cond_keys' compressed key)
+            def code(v):
+                v = np.asarray(v, dtype=np.int64)
+                return np.where(v < 128, v, np.minimum(128 + (v - 128) // 8, 255))
+            order = np.lexsort((code(rc.min(1)), code(rc.max(1)), dist0))
         else:
             order = np.lexsort((mn, mx, dist0))
         raw, f, dist = raw0[order], np.ascontiguousarray(f0[order]), \
