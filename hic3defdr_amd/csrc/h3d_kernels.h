@@ -727,6 +727,11 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
   constexpr int kBrentBlock = brent_block<M>();
   __shared__ double wpart[kBrentBlock / 64];
   __shared__ int s_next, s_more;
+  // the NLL log's table in LDS: its lookup address depends on the value, so
+  // the load sits on every lgamma's dependency chain (a global / L1 round
+  // trip otherwise)
+  __shared__ LogTab s_tab[129];
+  for (int t = threadIdx.x; t < 129; t += kBrentBlock) s_tab[t] = kLogTab[t];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   while (true) {
     __syncthreads();  // s_next / s_st reuse
@@ -772,10 +777,10 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
           v[k] = (k < nr) ? s_pd[k * lds_px + i] : 0.0;
           w[k] = (k < nr && two) ? s_pd[k * lds_px + j] : 0.0;
         }
-        const double t0 = nll_pixel<M>(v, nr, kc);
+        const double t0 = nll_pixel<M>(v, nr, kc, s_tab);
         acc += t0;
         if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc);
+          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
           if (two) acc += t1;
         }
       }
@@ -788,10 +793,10 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
           v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
           w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
         }
-        const double t0 = nll_pixel<M>(v, nr, kc);
+        const double t0 = nll_pixel<M>(v, nr, kc, s_tab);
         acc += t0;
         if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc);
+          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
           if (two) acc += t1;
         }
       }

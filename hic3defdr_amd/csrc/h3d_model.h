@@ -458,23 +458,24 @@ H3D_HD NllConst nll_const(double delta, int n) {
 // halves the transcendental work of the NLL passes. Arguments: d_j + r >=
 // 1/101 - ... > 0 (r = 1/delta - 1 >= 1/0.99 - 1, pseudodata >= 0).
 template <int M>
-H3D_HD double nll_pixel(const double* d, int n, const NllConst& k) {
+H3D_HD double nll_pixel(const double* d, int n, const NllConst& k,
+                        const LogTab* tab = kLogTab) {
   double lg[M];
   double lnp = 0.0, prod = 1.0;
 #pragma unroll
   for (int j = 0; j < M; ++j) {
     double pj = 1.0;
-    lg[j] = (j < n) ? lgam_nll_parts(d[j] + k.r, &pj) : 0.0;
+    lg[j] = (j < n) ? lgam_nll_parts(d[j] + k.r, &pj, tab) : 0.0;
     prod *= pj;
     if ((j & 7) == 7 && j + 1 < M) {  // keep 8 factors per logarithm
-      lnp += log_fast(prod);
+      lnp += log_fast(prod, tab);
       prod = 1.0;
     }
   }
   const double z = np_sum<M>(d, n);
   double pz = 1.0;
-  const double lz = lgam_nll_parts(z + k.nr, &pz);
-  lnp += log_fast(prod * recip_nll(pz));
+  const double lz = lgam_nll_parts(z + k.nr, &pz, tab);
+  lnp += log_fast(prod * recip_nll(pz), tab);
   return np_sum<M>(lg, n) - lnp + k.lg_nr - lz - k.n_lg_r;
 }
 

@@ -337,11 +337,12 @@ constexpr int kLogTabShifted = 53;  // buckets 0..53: m_i < sqrt(1/2)
 // the atanh-series form it replaces (one reciprocal, 11 series terms). Used
 // by the NLL sums (finite x > 0 by construction) and, through
 // log_fast_checked, the incomplete-gamma prefactor.
-H3D_HD double log_fast(double x) {
+// (tab: the table's copy to read -- kLogTab, or k_brent's copy in LDS)
+H3D_HD double log_fast(double x, const LogTab* tab = kLogTab) {
   int e;
   const double m = frexp(x, &e);  // [0.5, 1)
   const int i = (int)((m - 0.5) * 256.0 + 0.5);  // 0..128
-  const LogTab tb = kLogTab[i];
+  const LogTab tb = tab[i];
   const double t = fma(m, tb.c, -1.0);
   double q = 1.0 / 7.0;
   q = hfma(q, t, -1.0 / 6.0);
@@ -460,7 +461,7 @@ H3D_HD double lgam_nll(double x) {
 // shift product (1 for x >= 10), so a caller summing several lgammas takes
 // ONE log of the combined product (nll_pixel: per pixel R_c + 1 lgammas, one
 // ln P instead of up to R_c + 1).
-H3D_HD double lgam_nll_parts(double x, double* P) {
+H3D_HD double lgam_nll_parts(double x, double* P, const LogTab* tab = kLogTab) {
 #if defined(__clang__)
 #pragma clang fp contract(fast)
 #endif
@@ -476,7 +477,7 @@ H3D_HD double lgam_nll_parts(double x, double* P) {
   *P = p;
   const double r = recip_nll(y), r2 = r * r;
   const double corr = r * stirling_nll(r2);
-  return (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
+  return (y - 0.5) * log_fast(y, tab) - y + kLogSqrt2Pi + corr;
 }
 
 // log(1 + x) - x (cephes log1pmx). For |x| < 0.5 cephes sums the Taylor
