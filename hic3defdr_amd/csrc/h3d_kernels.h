@@ -878,6 +878,8 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
   __shared__ SegState s_st;
   __shared__ double wpart[kGangThreads / 64];
   __shared__ int s_next, s_more, s_abort;
+  __shared__ LogTab s_tab[129];  // the NLL log's table, as k_brent
+  for (int t = threadIdx.x; t < 129; t += kGangThreads) s_tab[t] = kLogTab[t];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   while (true) {
     __syncthreads();  // s_next / s_st reuse
@@ -921,9 +923,9 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
           v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
           w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
         }
-        acc += nll_pixel<M>(v, nr, kc);
+        acc += nll_pixel<M>(v, nr, kc, s_tab);
         if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc);
+          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
           if (two) acc += t1;
         }
       }
@@ -1020,6 +1022,11 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
   int cond[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) cond[k] = (k < R) ? cond_of_rep[k] : -1;
+  // the logpmf rows' log table in LDS (16 lookups per pixel at R = 4, each
+  // on its term's dependency chain)
+  __shared__ LogTab s_tab[129];
+  for (int t = threadIdx.x; t < 129; t += blockDim.x) s_tab[t] = kLogTab[t];
+  __syncthreads();
   int fl_all = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1053,7 +1060,7 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
     }
     double pv, lv, m0, m1[CM];
     fl_all |= lrt_pixel<M, CM>(x, fv, a, cond, R, C, refit != 0, &pv, &lv, &m0,
-                               m1);
+                               m1, s_tab);
     p[i] = pv;
     llr[i] = lv;
     mu0[i] = m0;

@@ -371,7 +371,8 @@ H3D_HD double logpmf(double k, double m, double phi) {
 template <int M, int CM, typename TX>
 H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
                      const int* cond, int R, int C, bool refit, double* p,
-                     double* llr, double* mu0, double* mu1) {
+                     double* llr, double* mu0, double* mu1,
+                     const LogTab* tab = kLogTab) {
   int st = 0;
   // fit 0 is the null (every replicate), fit t = c + 1 condition c's
   // replicates: ONE runtime loop, so fit_mu is inlined once rather than CM + 1
@@ -422,9 +423,10 @@ H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
       const double xk = (double)x[k];
       const double r = 1.0 / a[k];
       const double m0k = *mu0 * f[k], m1k = m1 * f[k];
-      const double l0 = log_fast_checked(r + m0k), l1 = log_fast_checked(r + m1k);
-      tn.add(k, -r * l0 + xk * log_fast_checked(m0k) - xk * l0);
-      ta.add(k, -r * l1 + xk * log_fast_checked(m1k) - xk * l1);
+      const double l0 = log_fast_checked(r + m0k, tab);
+      const double l1 = log_fast_checked(r + m1k, tab);
+      tn.add(k, -r * l0 + xk * log_fast_checked(m0k, tab) - xk * l0);
+      ta.add(k, -r * l1 + xk * log_fast_checked(m1k, tab) - xk * l1);
     }
   }
   *llr = tn.sum() - ta.sum();

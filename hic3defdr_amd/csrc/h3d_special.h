@@ -359,9 +359,9 @@ H3D_HD double log_fast(double x, const LogTab* tab = kLogTab) {
 // is first replaced by 1 there and libm's values (-inf, inf, NaN) are
 // selected afterwards (the k_brent NLL keeps the unchecked form: the checks
 // cost it 8 %, r03 PMC)
-H3D_HD double log_fast_checked(double x) {
+H3D_HD double log_fast_checked(double x, const LogTab* tab = kLogTab) {
   const bool ok = x > 0.0 && x < INFINITY;
-  const double v = log_fast(ok ? x : 1.0);
+  const double v = log_fast(ok ? x : 1.0, tab);
   if (ok) return v;
   return (x == INFINITY) ? INFINITY : (x == 0.0) ? -INFINITY : NAN;
 }
