@@ -213,7 +213,7 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
                   int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
                   SegState* st, const int* seg_flags, double* result, int* queue,
                   const int32_t* gate_meta = nullptr, int live_min = 0,
-                  const int* gang_abort = nullptr) {
+                  const int* gang_abort = nullptr, bool queue_zeroed = false) {
   ProfScope ps(ctx, "disp_nll", 0);
   auto k = k_brent<M>;
   constexpr int kBrentBlock = brent_block<M>();
@@ -234,7 +234,7 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
   // (M >= 16: 512-thread workgroups, two per CU -- staging would halve that)
   const size_t lds_bytes = M <= 8 ? (size_t)ctx->brent_lds_kb * 1024 : 0;
   const int64_t lds_px = (int64_t)(lds_bytes / (8 * (size_t)M));
-  (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
+  if (!queue_zeroed) (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), lds_px ? lds_px * 8 * M : 0,
                      ctx->stream, pd, n, seg_start, S, C, rep_idx, n_rep, st, seg_flags,
                      result, queue, ctx->work_count, lds_px, gate_meta, live_min, gang_abort);
@@ -383,9 +383,9 @@ void launch_brent_gang(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t*
                        int S, int C, const int32_t* rep_idx, const int32_t* n_rep,
                        SegState* st, const int* seg_flags, double* result, int* queue,
                        const GangTables& g, const int32_t* gate_meta = nullptr,
-                       int live_max = 0) {
+                       int live_max = 0, bool queue_zeroed = false) {
   ProfScope ps(ctx, "disp_nll", 0);
-  (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
+  if (!queue_zeroed) (void)hipMemsetAsync(queue, 0, sizeof(int), ctx->stream);
   const int epoch = gang_next_epoch(ctx, g, S);
   const int grid = std::max(1, std::min(g.T, g.grid));
   hipLaunchKernelGGL(k_brent_gang<M>, dim3(grid), dim3(kGangThreads), 0, ctx->stream, pd,
@@ -898,10 +898,13 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   stamp("tables uploaded");
 
+  // the single-rank Brent kernels' work queues, zeroed by k_seg_update
+  int* d_queue = (int*)scratch(ctx, "brent_queue", 2 * sizeof(int));
+  if (!d_queue) return fail(H3D_ENOMEM, "brent queue");
   // initial active list
   hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                      d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
-                     d_res, d_meta, 1, 0, d_lpx, ctx->work_count);
+                     d_res, d_meta, 1, 0, d_lpx, ctx->work_count, d_queue);
   if (!ctx->h_meta) HIP_TRY(hipHostMalloc((void**)&ctx->h_meta, 32, hipHostMallocDefault));
   int32_t* h_meta = ctx->h_meta;
   const size_t res_bytes = (size_t)S * 8 + (size_t)S * sizeof(SegState) + 8;
@@ -924,9 +927,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     // search in-kernel, then k_seg_update rebuilds the equalize list. The
     // host polls the live-segment count every `batch` iterations (an
     // iteration with nothing to do costs three empty launches).
-    int* d_queue = (int*)scratch(ctx, "brent_queue", sizeof(int));
     int64_t* d_seg = (int64_t*)scratch(ctx, "seg_start", (D + 1) * 8);
-    if (!d_queue || !d_seg) return fail(H3D_ENOMEM, "brent scratch");
+    if (!d_seg) return fail(H3D_ENOMEM, "brent scratch");
     if (n == 0) HIP_TRY(hipMemsetAsync(d_seg, 0, (D + 1) * 8, s));
     // H3D_BRENT: 1 (default) = gang searches (k_brent_gang) when the
     // segments are fewer than the CUs, 2 = always, 0 = one workgroup per
@@ -954,16 +956,17 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   dbg_launch("equalize");                                                                 \
   if (dual_on) {                                                                          \
     launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res,      \
-                     d_queue, d_meta, ctx->n_cu, gang.abort);                              \
+                     d_queue, d_meta, ctx->n_cu, gang.abort, true);                        \
     dbg_launch("k_brent (dual)");                                                         \
     launch_brent_gang<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, \
-                          d_queue, gang, d_meta, ctx->n_cu);                              \
+                          d_queue + 1, gang, d_meta, ctx->n_cu, true);                    \
     dbg_launch("k_brent_gang (dual)");                                                    \
   } else if (use_gang)                                                                    \
     launch_brent_gang<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, \
-                          d_queue, gang);                                                 \
+                          d_queue + 1, gang, nullptr, 0, true);                           \
   else                                                                                    \
-    launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res, d_queue)
+    launch_brent<MM>(ctx, pd, n, d_seg, S, C, d_repidx, d_nrep, d_st, d_flags, d_res,      \
+                     d_queue, nullptr, 0, nullptr, true)
         dbg_launch("before qcml iteration");
         if (mslot == 2) { H3D_QCML_ITER(2); }
         else if (mslot == 4) { H3D_QCML_ITER(4); }
@@ -975,7 +978,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
           ProfScope ps(ctx, "disp_update", 0);
           hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                              d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb, d_sle,
-                             d_res, d_meta, 0, 0, d_lpx, ctx->work_count);
+                             d_res, d_meta, 0, 0, d_lpx, ctx->work_count, d_queue);
         }
         ++rounds;
       }
@@ -1078,7 +1081,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         ProfScope ps(ctx, "disp_update", 0);
         hipLaunchKernelGGL(k_seg_update, dim3(1), dim3(1024), 0, s, d_st, d_total,
                            d_flags, S, C, d_nrep, d_scb, d_sce, d_list, d_slb,
-                           d_sle, d_res, d_meta, 0, 1, d_lpx, ctx->work_count);
+                           d_sle, d_res, d_meta, 0, 1, d_lpx, ctx->work_count, nullptr);
       }
       ++rounds;
     }

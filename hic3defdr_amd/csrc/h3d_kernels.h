@@ -550,7 +550,14 @@ static __global__ __launch_bounds__(1024) void k_seg_update(
     int32_t* __restrict__ seg_le, double* __restrict__ result,
     int32_t* __restrict__ meta /* [len, active, eq_len, live] */, int first, int step,
     const int64_t* __restrict__ seg_px /* this rank's pixels per segment */,
-    unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */) {
+    unsigned long long* __restrict__ work_count /* [equalize, nll] pixel-reps */,
+    int* __restrict__ brent_queue /* [k_brent, k_brent_gang] or null */) {
+  // the next iteration's Brent work queues start at 0 (two memset launches
+  // fewer per qcml iteration)
+  if (brent_queue && threadIdx.x == 0) {
+    brent_queue[0] = 0;
+    brent_queue[1] = 0;
+  }
   // Every cross-thread step is a wave shuffle tree plus one LDS slot per wave
   // (16 waves): no contended LDS atomics, two barriers per 1024 segments.
   constexpr int kW = 1024 / 64;
