@@ -133,9 +133,10 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
 
 // M = 16 / 24 / 32 (R <= M), CM >= C. Same arguments and outputs as k_lrt.
 template <int M, int CM>
-// 2 waves per SIMD (<= 256 registers): with the table log in its logpmf
-// rows the M = 32 instantiation grew into AGPRs at 1 wave (cfg4 lrt 22.7 ->
-// 31.0 ms, r03i), so the rows keep OCML log here
+// 2 waves per SIMD (<= 256 registers). (With the table log in its logpmf
+// rows the M = 32 instantiation grew into AGPRs at 1 wave -- cfg4 lrt 22.7
+// -> 31.0 ms, r03i --, while the rows still carried the cancelling prefix;
+// without it the rows take the table log from LDS, as k_lrt.)
 __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
     const int32_t* __restrict__ raw, const double* __restrict__ f,
     const int32_t* __restrict__ dist, const double* __restrict__ table,
@@ -146,6 +147,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
   constexpr int J = M / kGroup;
   const int lane = threadIdx.x & (kGroup - 1);
   const int base = (threadIdx.x & 63) & ~(kGroup - 1);  // group's first lane
+  __shared__ LogTab s_tab[129];  // the rows' log table, as k_lrt
+  for (int t = threadIdx.x; t < 129; t += blockDim.x) s_tab[t] = kLogTab[t];
+  __syncthreads();
   int cnd[J];
 #pragma unroll
   for (int s = 0; s < J; ++s) {
@@ -235,9 +239,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
       // the mean-free prefix of logpmf is common to the null and alt rows
       // and cancels in llr: left out, as k_lrt (lrt_pixel)
       const double m0k = m0 * fv[s], m1f = m1k * fv[s];
-      const double l0 = log(r + m0k), l1 = log(r + m1f);
-      tn[s] = -r * l0 + xk * log(m0k) - xk * l0;
-      ta[s] = -r * l1 + xk * log(m1f) - xk * l1;
+      const double l0 = log_fast_checked(r + m0k, s_tab);
+      const double l1 = log_fast_checked(r + m1f, s_tab);
+      tn[s] = -r * l0 + xk * log_fast_checked(m0k, s_tab) - xk * l0;
+      ta[s] = -r * l1 + xk * log_fast_checked(m1f, s_tab) - xk * l1;
     }
     const double lv = np_sum_g8<J>(tn, R, lane, base) - np_sum_g8<J>(ta, R, lane, base);
     fl_all |= st;
