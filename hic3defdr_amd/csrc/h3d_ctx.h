@@ -118,8 +118,10 @@ struct h3d_ctx {
   int brent_gang = 1;
   int gang_aborts = 0;  // gang waits that timed out (fell back to k_brent)
   // H3D_BRENT_LDS_KB: LDS per k_brent workgroup for the segment's staged
-  // head (0 = stream every evaluation from memory)
-  int brent_lds_kb = 144;
+  // head (0 = stream every evaluation from memory). With the log table in
+  // LDS too, r03am: 64 / 96 / 128 KB 2.62-2.66 ms of Brent per cfg2 step,
+  // 80 / 112 / 144 KB 2.73-2.80 (the replicate rows' LDS stride), 0 KB 2.67
+  int brent_lds_kb = 128;
   // k_brent_gang tag epoch (tags carry it, so they need no clearing between
   // launches) and the tag buffer it is valid for
   int gang_epoch = 0;
