@@ -258,8 +258,9 @@ def cpu_baseline_run(full_bins, sample_bins, dmax, seed=123, full_runs=1):
             'median_s': fixed['median_s'], 'runs_s': fixed['runs_s'],
             'sample': '1 synthetic chrom of %d bins (seed %d), dmax %d, 4 '
                       'reps 2+2: %d disp pixels -- the headline workload '
-                      'shape; %d run(s)' % (full_bins or sample_bins, seed,
-                                            dmax, n_full, full_runs),
+                      'shape; median of %d run(s)' % (
+                          full_bins or sample_bins, seed, dmax, n_full,
+                          full_runs),
             'fallback_fixed_on_sample': dict(s_fixed, pixels=len(
                 sample['raw'])),
             'faithful': {
@@ -304,6 +305,68 @@ def sample_parity(ctx, sample, dmax):
         res['identical_calls_q<0.05_%s' % name] = bool(
             np.array_equal(qg < 0.05, qo < 0.05))
     return res
+
+
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+
+
+def parity_vs_reference(ctx, o, n, bins, dmax, seed):
+    """The metric's second half, max-|dq| vs reference: the timed step's own
+    p-values (left in HBM by the last timed step), BH on the device, against
+    the REFERENCE's end-to-end run on this same chromosome
+    (tests/golden/full_cfg2.npz: the reference's prepare_data +
+    estimate_disp + lrt + bh, 50 k seeded sample pixels and the 2,000
+    smallest p-values) and against the reference's own results under six
+    pixel orders of its input (cfg2_spread.npz: the reference is only
+    defined up to that spread). None unless the workload is that chromosome."""
+    try:
+        g = np.load(os.path.join(GOLDEN, 'full_cfg2.npz'))
+        sp = np.load(os.path.join(GOLDEN, 'cfg2_spread.npz'))
+    except OSError:
+        return None
+    if (int(g['meta_bins']), int(g['meta_dmax']), int(g['meta_seed'])) != \
+            (bins, dmax, seed) or int(g['n_disp_pixels']) != n:
+        return None
+    ctx.bh_dev(o['p'].data_ptr(), n, o['q'].data_ptr())
+    p, q = o['p'].cpu().numpy(), o['q'].cpu().numpy()
+    s, t = g['sample_idx'], g['top_idx']
+
+    def rel(a, b):
+        return float(np.max(np.abs(a - b) / np.abs(b)))
+
+    def dq(a, b):
+        return float(np.max(np.abs(a - b)))
+    out = {'reference': 'tests/golden/full_cfg2.npz (make_golden.py '
+                        'run_full_cfg2: the reference run on this chromosome)',
+           'pixels_compared': int(len(s) + len(t)),
+           'max_abs_dq_vs_reference': max(dq(q[s], g['q']),
+                                          dq(q[t], g['top_q'])),
+           'max_rel_dq_vs_reference': max(rel(q[s], g['q']),
+                                          rel(q[t], g['top_q'])),
+           'max_rel_dp_vs_reference': max(rel(p[s], g['p']),
+                                          rel(p[t], g['top_p'])),
+           'identical_calls': all(
+               np.array_equal(np.where(q < fdr)[0], g['calls_%g' % fdr])
+               for fdr in (0.01, 0.05, 0.1))}
+    near = []
+    for k in sp['perms']:
+        near.append((max(rel(p[s], sp['p_sample__%d' % k]),
+                         rel(p[t], sp['p_top__%d' % k])),
+                     max(dq(q[s], sp['q_sample__%d' % k]),
+                         dq(q[t], sp['q_top__%d' % k])), int(k)))
+    best = min(near)
+    out['nearest_reference_order'] = {
+        'order': best[2], 'max_rel_dp': best[0], 'max_abs_dq': best[1],
+        'note': 'the reference re-run with the pixels of every segment in '
+                'another order (cfg2_spread.npz, 6 orders incl. its own)'}
+    out['reference_own_spread'] = {
+        'max_rel_dp': max(rel(sp['p_sample__%d' % k], g['p'])
+                          for k in sp['perms']),
+        'max_abs_dq': max(dq(sp['q_sample__%d' % k], g['q'])
+                          for k in sp['perms']),
+        'note': 'how far the reference moves itself under those orders '
+                '(sample pixels)'}
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -615,6 +678,9 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
                 'distance re-shard: all_to_all of the disp pixels, in-kernel '
                 'Brent per rank, table all-reduce' if by_dist
                 else 'per-pass NLL all-reduce over RCCL'), 'weak')
+        if world == 1:
+            out['parity_vs_reference'] = parity_vs_reference(
+                ctx, o, n, args.bins, args.dmax, rank)
         if cpu is not None:
             out['cpu_baseline'] = cpu[0]
             out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
@@ -751,6 +817,8 @@ def main():
                     help='the faithful CPU row sample')
     ap.add_argument('--cpu-full-bins', type=int, default=20000,
                     help='the fallback-fixed CPU row (0: the sample)')
+    ap.add_argument('--cpu-full-runs', type=int, default=3,
+                    help='runs of the full-chromosome CPU row (median)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
     ap.add_argument('--noop-reduce', action='store_true',
@@ -772,7 +840,8 @@ def main():
     cpu = None
     if world == 1 and config == 'cfg2' and not args.no_cpu_baseline:
         cpu = cpu_baseline_run(args.cpu_full_bins, args.cpu_bins,
-                               args.dmax)   # before the GPU
+                               args.dmax, full_runs=args.cpu_full_runs)
+        # (before the GPU: the pool forks)
     import torch
     torch.cuda.set_device(local)
     dist = None

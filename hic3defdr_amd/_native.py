@@ -32,7 +32,8 @@ EXPORTS = [
     'h3d_bh_ctx', 'h3d_bh_dev', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
     'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
     'h3d_estimate_disp_dev', 'h3d_bh_sort_dev', 'h3d_bh_scan_dev',
-    'h3d_bh_finish_dev',
+    'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
+    'h3d_disp_pixels_dev', 'h3d_table_gather_dev',
 ]
 
 
@@ -88,6 +89,13 @@ def load_library(path=None):
             'h3d_set_stream': (_I, [_P, _P]),
             'h3d_union_count': (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
             'h3d_union_fill': (_I, [_P, _P, _P, _P, _P, _I64]),
+            'h3d_union_fill_dev': (_I, [_P, _P, _P, _P, _P, _I64, _P, _P, _P,
+                                        _P]),
+            'h3d_size_factors_dev': (_I, [_P, _P, _P, _I64, _I, _I, _I, _P,
+                                          _P]),
+            'h3d_disp_pixels_dev': (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _P,
+                                         _I64, _I, _I64, _P, _P, _P]),
+            'h3d_table_gather_dev': (_I, [_P, _P, _I, _I, _P, _I64, _P]),
             'h3d_size_factors_cmor': (_I, [_P, _P, _P, _I64, _I, _I, _P]),
             'h3d_size_factors': (_I, [_P, _P, _P, _I64, _I, _I, _I, _P]),
             'h3d_disp_per_dist': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I,
@@ -226,11 +234,13 @@ class Context(object):
                'h3d_set_stream')
 
     # -- prepare_data -------------------------------------------------------
-    def sparse_union(self, csrs, bias, dist_max):
+    def sparse_union(self, csrs, bias, dist_max, device_alloc=None):
         """csrs: list of canonical CSR matrices (scipy or `CSR`, n_bins x
         n_bins); bias
         (n_bins, R) filtered. Returns row, col (int32), raw (int64 (n, R)),
-        balanced (float64 (n, R))."""
+        balanced (float64 (n, R)). ``device_alloc(n, R)``, when given,
+        returns device pointers (row, col, raw int32, balanced; any may be
+        None) that also receive the union (h3d_union_fill_dev)."""
         R = len(csrs)
         n_bins = bias.shape[0]
         keep = []
@@ -255,10 +265,50 @@ class Context(object):
         col = np.empty(n, dtype=np.int32)
         raw = np.empty((n, R), dtype=np.int64)
         bal = np.empty((n, R), dtype=np.float64)
-        _check(self.lib.h3d_union_fill(self.handle, _ptr(row), _ptr(col),
-                                       _ptr(raw), _ptr(bal), n),
-               'h3d_union_fill')
+        if device_alloc is None:
+            _check(self.lib.h3d_union_fill(self.handle, _ptr(row), _ptr(col),
+                                           _ptr(raw), _ptr(bal), n),
+                   'h3d_union_fill')
+        else:
+            d = device_alloc(n, R)
+            _check(self.lib.h3d_union_fill_dev(
+                self.handle, _ptr(row), _ptr(col), _ptr(raw), _ptr(bal), n,
+                *[_P(v) if v else None for v in d]), 'h3d_union_fill_dev')
         return row, col, raw, bal
+
+    def size_factors_dev(self, d_balanced, dist, n, R, norm='conditional_mor',
+                         n_bins=0, d_sf_out=None):
+        """size_factors on a device balanced (n, R); the result on the host
+        and, with ``d_sf_out``, in that device buffer ((n, R) or (R,))."""
+        if norm not in H3D_NORM:
+            raise ValueError('unknown norm %r' % (norm,))
+        cond = norm.startswith('conditional')
+        dist = _c(dist, np.int32) if cond else None
+        out = np.empty((n, R) if cond else R, dtype=np.float64)
+        _check(self.lib.h3d_size_factors_dev(
+            self.handle, _P(d_balanced), _ptr(dist), n, R, H3D_NORM[norm],
+            int(n_bins or 0), _ptr(out), _P(d_sf_out) if d_sf_out else None),
+            'h3d_size_factors_dev')
+        return out
+
+    def disp_pixels_dev(self, d_row, d_col, d_raw, d_sf, sf_per_rep, bias,
+                        d_disp_idx, n, R, n_disp, d_raw_out, d_f_out,
+                        d_dist_out):
+        """A chromosome's disp pixels on the device (h3d_disp_pixels_dev):
+        raw (n_disp, R) int32, f = bias[row] * bias[col] * sf, dist."""
+        bias = _c(bias, np.float64)
+        _check(self.lib.h3d_disp_pixels_dev(
+            self.handle, _P(d_row), _P(d_col), _P(d_raw), _P(d_sf),
+            int(bool(sf_per_rep)), _ptr(bias), bias.shape[0], _P(d_disp_idx),
+            n, R, n_disp, _P(d_raw_out) if d_raw_out else None,
+            _P(d_f_out) if d_f_out else None,
+            _P(d_dist_out) if d_dist_out else None), 'h3d_disp_pixels_dev')
+
+    def table_gather_dev(self, d_tables, D, C, d_dist, n, d_out):
+        """disp = tables[dist] on the device (h3d_table_gather_dev)."""
+        _check(self.lib.h3d_table_gather_dev(self.handle, _P(d_tables), D, C,
+                                             _P(d_dist), n, _P(d_out)),
+               'h3d_table_gather_dev')
 
     def size_factors_cmor(self, balanced, dist, n_bins):
         balanced = _c(balanced, np.float64)

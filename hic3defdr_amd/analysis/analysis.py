@@ -40,6 +40,9 @@ from hic3defdr_amd.util.printing import eprint
 
 NATIVE_NORMS = tuple(_native.H3D_NORM)
 NATIVE_ESTIMATORS = ('qcml',)
+# H3D_RESIDENT=0: prepare_data does not keep the union in HBM (estimate_disp
+# and lrt then upload it from the outdir files, as a new process would)
+_KEEP_RESIDENT = os.environ.get('H3D_RESIDENT', '1') != '0'
 
 
 def _canonical_csr(fname):
@@ -113,13 +116,28 @@ class AnalyzingHiC3DeFDR(object):
                                [p.replace('<chrom>', chrom)
                                 for p in self.raw_npz_patterns]))
         ctx = self._ctx()
+        res = self._resident() if _KEEP_RESIDENT else None
+        holder = {}
         eprint('  computing union pixel set', skip=not verbose)
-        row, col, raw, balanced = ctx.sparse_union(mats, bias,
-                                                   self.dist_thresh_max)
+        try:
+            row, col, raw, balanced = ctx.sparse_union(
+                mats, bias, self.dist_thresh_max,
+                device_alloc=res.union_alloc(holder) if res else None)
+        except _native.H3DError:
+            if not holder:
+                raise
+            # counts beyond int32: no device copy (the disp / lrt kernels
+            # reject such counts anyway, as before)
+            res, holder = None, {}
+            row, col, raw, balanced = ctx.sparse_union(mats, bias,
+                                                       self.dist_thresh_max)
         eprint('  computing size factors', skip=not verbose)
         dist = col - row
         # analysis.py:104-108: conditional norms see the distances
-        size_factors = ctx.size_factors(balanced, dist, norm, n_bins or 0)
+        if res is not None and 'bal' in holder:
+            size_factors = res.size_factors(holder, dist, norm, n_bins or 0)
+        else:
+            size_factors = ctx.size_factors(balanced, dist, norm, n_bins or 0)
         scaled = balanced / size_factors
         design = np.asarray(self.design, dtype=bool)
         mean = np.dot(scaled, design) / np.sum(design, axis=0)
@@ -132,12 +150,12 @@ class AnalyzingHiC3DeFDR(object):
             loop_idx = pixel_membership(row[disp_idx], col[disp_idx], cl)
             self.save_data(loop_idx, 'loop_idx', chrom)
         eprint('  saving data to disk', skip=not verbose)
-        self.save_data(row, 'row', chrom)
-        self.save_data(col, 'col', chrom)
-        self.save_data(raw, 'raw', chrom)
-        self.save_data(size_factors, 'size_factors', chrom)
-        self.save_data(scaled, 'scaled', chrom)
-        self.save_data(disp_idx, 'disp_idx', chrom)
+        for name, a in (('row', row), ('col', col), ('raw', raw),
+                        ('size_factors', size_factors), ('scaled', scaled),
+                        ('disp_idx', disp_idx)):
+            self._save_npy(self._npy(name, chrom), a, owned=True)
+        if res is not None and 'sf' in holder:
+            res.keep(chrom, holder, disp_idx, bias)
 
     # ------------------------------------------------------------------
     def _f_and_dist(self, chroms=None):
@@ -169,7 +187,20 @@ class AnalyzingHiC3DeFDR(object):
         return np.concatenate(raws), np.concatenate(fs), \
             np.concatenate(dists), offsets
 
-    def _disp_per_dist_sharded(self, sh, raw, f, dist, C, D):
+    def _resident(self):
+        """The device copy of this object's stages (analysis/resident.py)."""
+        r = self.__dict__.get('_dev_resident')
+        if r is None or r.ctx is not self._ctx():
+            try:
+                from hic3defdr_amd.analysis.resident import Resident
+                r = Resident(self)
+            except ImportError as e:
+                raise _native.H3DError(
+                    'the GPU path needs torch (device memory): %s' % e)
+            self.__dict__['_dev_resident'] = r
+        return r
+
+    def _disp_per_dist_sharded(self, t_raw, t_f, t_dist, C, D):
         """estimate_disp's per-(distance, condition) qcml over every rank's
         pixels: re-sharded by distance (parallel.disp_per_dist_by_distance:
         one all_to_all, the single-GPU driver per rank, one all-reduce of the
@@ -180,10 +211,6 @@ class AnalyzingHiC3DeFDR(object):
         ctx = self._ctx()
         dev = torch.device('cuda', ctx.device)
         torch.cuda.set_device(dev)
-        t_raw = torch.from_numpy(np.ascontiguousarray(
-            raw, dtype=np.int32)).to(dev)
-        t_f = torch.from_numpy(np.ascontiguousarray(f)).to(dev)
-        t_d = torch.from_numpy(np.ascontiguousarray(dist, dtype=np.int32)).to(dev)
         torch.cuda.synchronize(dev)
         # a real stream shared by libh3d and the collective: torch's default
         # stream has handle 0, which h3d_set_stream reads as "the ctx's own
@@ -194,94 +221,180 @@ class AnalyzingHiC3DeFDR(object):
             with torch.cuda.stream(stream):
                 if os.environ.get('H3D_DISP_SHARD') != 'pass':
                     return parallel.disp_per_dist_by_distance(
-                        ctx, t_raw, t_f, t_d, self._cond_of_rep(), C, D)
+                        ctx, t_raw, t_f, t_dist, self._cond_of_rep(), C, D)
                 return ctx.disp_per_dist_dev(
-                    t_raw.data_ptr(), t_f.data_ptr(), t_d.data_ptr(), len(raw),
-                    self.design.shape[0], self._cond_of_rep(), C, D,
-                    reduce=parallel.make_allreduce())
+                    t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
+                    t_raw.shape[0], self.design.shape[0], self._cond_of_rep(),
+                    C, D, reduce=parallel.make_allreduce())
         finally:
             stream.synchronize()
             ctx.set_stream(None)
 
     def estimate_disp(self, estimator='qcml', frac=None, auto_frac_factor=15.,
                       weighted_lowess=True, n_threads=-1):
-        """Reference ``analysis.py:135-223``."""
+        """Reference ``analysis.py:135-223``. The native estimator runs on
+        the device end to end (resident.py): the disp pixels of this rank's
+        chromosomes built in HBM, qcml per (distance, condition), the
+        smoothed tables and ``disp = table[dist]``; disp goes to the outdir
+        (write-behind) and stays resident for lrt."""
         eprint('estimating dispersion')
         sh = self._shards()
-        raw, f, dist, offsets = self._f_and_dist(sh.mine)
+        design = np.asarray(self.design, dtype=bool)
+        R, C = design.shape
+        D = self.dist_thresh_max + 1
+        if callable(estimator) or estimator not in NATIVE_ESTIMATORS:
+            if sh.sharded:
+                raise NotImplementedError(
+                    'sharded estimate_disp implements %s' % (NATIVE_ESTIMATORS,))
+            if not callable(estimator):
+                raise NotImplementedError(
+                    'estimator=%r: the reference divides its int64 raw slice '
+                    'in place for cml/mme (dispersion.py:76,129) and raises; '
+                    'the GPU path implements %s' % (estimator,
+                                                    NATIVE_ESTIMATORS))
+            return self._estimate_disp_callable(estimator, frac,
+                                                auto_frac_factor,
+                                                weighted_lowess)
+        import torch
+        res = self._resident()
+        ctx = self._ctx()
+        cond = self._cond_of_rep()
+        t_raw, t_f, t_dist, offsets = res.disp_pixels(sh.mine, R)
+        n = int(t_raw.shape[0])
+        t_tab = torch.empty((D, C), dtype=torch.float64, device=res.dev)
+        if sh.sharded:
+            disp_per_dist = self._disp_per_dist_sharded(t_raw, t_f, t_dist, C,
+                                                        D)
+            t_dpd = torch.from_numpy(np.ascontiguousarray(disp_per_dist)).to(
+                res.dev)
+            torch.cuda.synchronize(res.dev)
+            ctx.disp_tables_dev(t_dpd.data_ptr(), D, C, t_tab.data_ptr(),
+                                weighted=weighted_lowess, frac=frac,
+                                auto_frac_factor=auto_frac_factor)
+        else:
+            torch.cuda.synchronize(res.dev)
+            disp_per_dist = ctx.estimate_disp_dev(
+                t_raw.data_ptr() if n else None, t_f.data_ptr() if n else None,
+                t_dist.data_ptr() if n else None, n, R, cond, C, D,
+                t_tab.data_ptr(), weighted=weighted_lowess, frac=frac,
+                auto_frac_factor=auto_frac_factor)
+        eprint('  fitting distance vs dispersion relationship')
+        t_disp = torch.empty((n, C), dtype=torch.float64, device=res.dev)
+        # settles the device smoother (a degenerate fit is redone on the host)
+        ctx.table_gather_dev(t_tab.data_ptr(), D, C,
+                             t_dist.data_ptr() if n else None, n,
+                             t_disp.data_ptr() if n else None)
+        # (table_gather_dev returns with the ctx stream drained)
+        tables = t_tab.cpu().numpy()
+        disp = t_disp.cpu().numpy()
+        del t_disp
+        if sh.rank == 0:
+            for c, cond_name in enumerate(self.design.columns):
+                self.save_disp_fn(cond_name, DispFn(tables[:, c],
+                                                    disp_per_dist[:, c],
+                                                    weighted=weighted_lowess))
+        eprint('  saving estimated dispersions to disk')
+        for i, chrom in enumerate(sh.mine):
+            self._save_npy(self._npy('disp', chrom),
+                           disp[offsets[i]:offsets[i + 1]], owned=True)
+        if sh.rank == 0:
+            self.save_data(disp_per_dist, 'disp_per_dist')
+        res.start_session(sh.mine, t_raw, t_f, t_dist, offsets, t_tab, D, C)
+        sh.barrier()
+
+    def _estimate_disp_callable(self, estimator, frac, auto_frac_factor,
+                                weighted_lowess):
+        """A user-supplied Python estimator runs where the user wrote it, on
+        the host (analysis.py:164-165, :196-206)."""
         design = np.asarray(self.design, dtype=bool)
         C = design.shape[1]
         D = self.dist_thresh_max + 1
-        if sh.sharded:
-            if estimator not in NATIVE_ESTIMATORS:
-                raise NotImplementedError(
-                    'sharded estimate_disp implements %s' % (NATIVE_ESTIMATORS,))
-            disp_per_dist = self._disp_per_dist_sharded(sh, raw, f, dist, C, D)
-        elif callable(estimator):
-            # a user-supplied Python estimator runs where the user wrote it
-            disp_per_dist = np.zeros((D, C))
-            for c in range(C):
-                for d in range(D):
-                    sel = dist == d
-                    rs = raw[sel][:, design[:, c]]
-                    fs = f[sel][:, design[:, c]]
-                    disp_per_dist[d, c] = np.nan if not rs.size else \
-                        estimator(rs, f=fs)
-        elif estimator in NATIVE_ESTIMATORS:
-            disp_per_dist = self._ctx().disp_per_dist(
-                raw, f, dist, self._cond_of_rep(), C, D, estimator=estimator)
-        else:
-            raise NotImplementedError(
-                'estimator=%r: the reference divides its int64 raw slice in '
-                'place for cml/mme (dispersion.py:76,129) and raises; the GPU '
-                'path implements %s' % (estimator, NATIVE_ESTIMATORS))
-        disp = np.zeros((len(raw), C))
+        raw, f, dist, offsets = self._f_and_dist()
+        disp_per_dist = np.zeros((D, C))
+        for c in range(C):
+            for d in range(D):
+                sel = dist == d
+                rs = raw[sel][:, design[:, c]]
+                fs = f[sel][:, design[:, c]]
+                disp_per_dist[d, c] = np.nan if not rs.size else \
+                    estimator(rs, f=fs)
         eprint('  fitting distance vs dispersion relationship')
         tables = _native.disp_tables(disp_per_dist, weighted=weighted_lowess,
                                      frac=frac,
                                      auto_frac_factor=auto_frac_factor)
+        disp = np.zeros((len(raw), C))
         for c, cond in enumerate(self.design.columns):
-            table = tables[:, c]
-            disp[:, c] = table[dist]
-            if sh.rank == 0:
-                self.save_disp_fn(cond, DispFn(table, disp_per_dist[:, c],
-                                               weighted=weighted_lowess))
+            disp[:, c] = tables[:, c][dist]
+            self.save_disp_fn(cond, DispFn(tables[:, c], disp_per_dist[:, c],
+                                           weighted=weighted_lowess))
         eprint('  saving estimated dispersions to disk')
-        for i, chrom in enumerate(sh.mine):
-            self.save_data(disp[offsets[i]:offsets[i + 1]], 'disp', chrom)
-        if sh.rank == 0:
-            self.save_data(disp_per_dist, 'disp_per_dist')
-        sh.barrier()
+        for i, chrom in enumerate(self.chroms):
+            self._save_npy(self._npy('disp', chrom),
+                           disp[offsets[i]:offsets[i + 1]], owned=True)
+        self.save_data(disp_per_dist, 'disp_per_dist')
 
     # ------------------------------------------------------------------
     def lrt(self, chrom=None, refit_mu=True, n_threads=-1, verbose=True):
-        """Reference ``analysis.py:225-284``."""
-        if chrom is None:
-            sh = self._shards()
-            for c in sh.mine:
-                self.lrt(chrom=c, refit_mu=refit_mu, verbose=verbose)
-            sh.barrier()
-            return
-        eprint('running LRT for chrom %s' % chrom, skip=not verbose)
-        bias = self.load_bias(chrom)
-        size_factors = self.load_data('size_factors', chrom)
-        disp_idx = self.load_data('disp_idx', chrom)
-        row = self.load_data('row', chrom, idx=disp_idx)
-        col = self.load_data('col', chrom, idx=disp_idx)
-        raw = self.load_data('raw', chrom, idx=disp_idx)
-        disp = self.load_data('disp', chrom)
-        if len(size_factors.shape) == 2:
-            f = _pixel_factors(bias, row, col, size_factors[disp_idx, :])
+        """Reference ``analysis.py:225-284``, on the device: over
+        estimate_disp's resident pixels and tables in one launch while its
+        disp files are current (resident.py), otherwise per chromosome from
+        the outdir (the per-pixel disp as the reference loads it)."""
+        sh = self._shards() if chrom is None else None
+        chroms = sh.mine if chrom is None else [chrom]
+        res = self._resident()
+        sess = res.lrt_session(chroms) if chrom is None else None
+        if sess is not None:
+            for c in chroms:
+                eprint('running LRT for chrom %s' % c, skip=not verbose)
+            self._lrt_run(res, chroms, sess['raw'], sess['f'], sess['dist'],
+                          sess['offsets'], refit_mu, table=sess['tables'])
         else:
-            f = _pixel_factors(bias, row, col, size_factors)
-        p, llr, mu0, mu1, _ = self._ctx().lrt(raw, f, None, disp,
-                                              self._cond_of_rep(),
-                                              refit_mu=refit_mu,
-                                              want_disp=False)
-        self.save_data(p, 'pvalues', chrom)
-        self.save_data(llr, 'llr', chrom)
-        self.save_data(mu0, 'mu_hat_null', chrom)
-        self.save_data(mu1, 'mu_hat_alt', chrom)
+            for c in chroms:
+                eprint('running LRT for chrom %s' % c, skip=not verbose)
+                t_raw, t_f, t_dist, offsets = res.disp_pixels([c],
+                                                              len(self.design))
+                disp = self.load_data('disp', c)
+                self._lrt_run(res, [c], t_raw, t_f, None, offsets, refit_mu,
+                              disp=disp)
+        if sh is not None:
+            sh.barrier()
+
+    def _lrt_run(self, res, chroms, t_raw, t_f, t_dist, offsets, refit_mu,
+                 table=None, disp=None):
+        """One LRT launch over the concatenated disp pixels of ``chroms``:
+        with the device ``table`` (D, C) and t_dist, or the per-pixel
+        ``disp`` (n, C) from the outdir; the four outputs saved per
+        chromosome (write-behind)."""
+        import torch
+        ctx = self._ctx()
+        n = int(t_raw.shape[0])
+        C = self.design.shape[1]
+        if n:
+            tp = torch.empty((3, n), dtype=torch.float64, device=res.dev)
+            t1 = torch.empty((n, C), dtype=torch.float64, device=res.dev)
+            ptrs = (tp[0].data_ptr(), tp[1].data_ptr(), tp[2].data_ptr(),
+                    t1.data_ptr())
+            if table is not None:
+                ctx.lrt_dev_tab(t_raw.data_ptr(), t_f.data_ptr(),
+                                t_dist.data_ptr(), table.data_ptr(),
+                                table.shape[0], n, len(self.design),
+                                self._cond_of_rep(), *ptrs, refit_mu=refit_mu)
+            else:
+                ctx.lrt_dev(t_raw.data_ptr(), t_f.data_ptr(), None, disp, n,
+                            len(self.design), self._cond_of_rep(), *ptrs,
+                            refit_mu=refit_mu)
+            # (the lrt calls return with the ctx stream drained)
+            h3, mu1 = tp.cpu().numpy(), t1.cpu().numpy()
+            del tp, t1
+        else:
+            h3, mu1 = np.empty((3, 0)), np.empty((0, C))
+        p, llr, mu0 = h3
+        for i, c in enumerate(chroms):
+            a, b = offsets[i], offsets[i + 1]
+            self._save_npy(self._npy('pvalues', c), p[a:b], owned=True)
+            self._save_npy(self._npy('llr', c), llr[a:b], owned=True)
+            self._save_npy(self._npy('mu_hat_null', c), mu0[a:b], owned=True)
+            self._save_npy(self._npy('mu_hat_alt', c), mu1[a:b], owned=True)
 
     # ------------------------------------------------------------------
     def bh(self):

@@ -1,0 +1,223 @@
+"""The product path's device-resident copy of a HiC3DeFDR object's stage data.
+
+The reference's stages hand their data over through the outdir only
+(prepare_data writes row / col / raw / size_factors / disp_idx,
+``analysis.py:128-133``; estimate_disp reads them back and rebuilds
+``f = bias[row] * bias[col] * size_factors``, ``:169-183``; lrt reads them
+and ``disp`` again and rebuilds ``f``, ``:261-275``). The outdir contract is
+kept -- every file is written (core.py's write-behind queue) -- but within
+one object the data also stays in HBM:
+
+* prepare_data leaves each chromosome's union (row, col, raw as int32, size
+  factors, disp_idx) in device buffers (``h3d_union_fill_dev``,
+  ``h3d_size_factors_dev``), so nothing is re-read or re-uploaded;
+* estimate_disp builds the disp pixels of all its chromosomes on the device
+  (``h3d_disp_pixels_dev``: compaction by disp_idx, f in numpy's product
+  order) -- from the resident union, or uploaded from the outdir files when
+  another process prepared them -- and runs qcml, the smoother and
+  ``disp = table[dist]`` there (``h3d_estimate_disp_dev``,
+  ``h3d_table_gather_dev``);
+* lrt runs over estimate_disp's resident pixels and device tables in one
+  launch (``h3d_lrt_dev_tab``) while the disp files it would read are the
+  ones estimate_disp wrote; otherwise per chromosome from the files.
+
+A resident entry is used only while the outdir files it mirrors are the
+ones it was made from (core.CoreHiC3DeFDR.is_current, or the file stamps
+taken when it was loaded from disk) and the bias files are unchanged, so
+edits of the outdir are always seen. Device buffers are torch tensors (the
+allocator); every computation on them is libh3d's.
+"""
+import os
+
+import numpy as np
+
+from hic3defdr_amd import _native
+
+
+def _stamp(fname):
+    try:
+        st = os.stat(fname)
+    except OSError:
+        return None
+    return (st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns)
+
+
+class ChromDev(object):
+    """One chromosome's union pixels on the device."""
+
+    def __init__(self, row, col, raw, sf, sf_per_rep, disp_idx, n_disp, bias,
+                 files):
+        self.row, self.col, self.raw = row, col, raw
+        self.sf, self.sf_per_rep = sf, sf_per_rep
+        self.disp_idx, self.n_disp = disp_idx, n_disp
+        self.bias = bias      # host (n_bins, R), bias_thresh-filtered
+        self.files = files    # fname -> ('ours', generation) / ('disk', stamp)
+        self.n = int(row.shape[0])
+
+
+class Resident(object):
+    """The device copy of one object's stages (see the module docstring)."""
+
+    STAGES = ('row', 'col', 'raw', 'size_factors', 'disp_idx')
+
+    def __init__(self, h):
+        import torch
+        self.torch = torch
+        self.h = h
+        self.ctx = h._ctx()
+        self.dev = torch.device('cuda', self.ctx.device)
+        self.chroms = {}
+        self.session = None
+
+    # -- validity --------------------------------------------------------
+    def _current(self, files):
+        for fname, (kind, tok) in files.items():
+            if kind == 'ours':
+                if self.h.write_generation(fname) != tok or \
+                        not self.h.is_current(fname):
+                    return False
+            elif _stamp(fname) != tok:
+                return False
+        return True
+
+    def _token(self, fname):
+        """('ours', generation) for an outdir file this object wrote and
+        that is still that write, else ('disk', file stamp)."""
+        if self.h.is_current(fname):
+            return ('ours', self.h.write_generation(fname))
+        return ('disk', _stamp(fname))
+
+    def _bias_stamps(self, chrom):
+        return {f: ('disk', _stamp(f)) for f in
+                (p.replace('<chrom>', chrom) for p in self.h.bias_patterns)}
+
+    # -- prepare_data ----------------------------------------------------
+    def union_alloc(self, holder):
+        """device_alloc for Context.sparse_union: the union's device
+        buffers, kept in ``holder``."""
+        torch = self.torch
+
+        def alloc(n, R):
+            holder['row'] = torch.empty(n, dtype=torch.int32, device=self.dev)
+            holder['col'] = torch.empty(n, dtype=torch.int32, device=self.dev)
+            holder['raw'] = torch.empty((n, R), dtype=torch.int32,
+                                        device=self.dev)
+            holder['bal'] = torch.empty((n, R), dtype=torch.float64,
+                                        device=self.dev)
+            return tuple(holder[k].data_ptr() if n else None
+                         for k in ('row', 'col', 'raw', 'bal'))
+        return alloc
+
+    def size_factors(self, holder, dist, norm, n_bins):
+        """Size factors on the resident balanced: host copy returned, device
+        copy kept in ``holder['sf']``; balanced is released."""
+        torch = self.torch
+        n, R = holder['bal'].shape
+        cond = norm.startswith('conditional')
+        holder['sf'] = torch.empty((n, R) if cond else R, dtype=torch.float64,
+                                   device=self.dev)
+        sf = self.ctx.size_factors_dev(
+            holder['bal'].data_ptr() if n else None, dist, n, R, norm, n_bins,
+            d_sf_out=holder['sf'].data_ptr() if holder['sf'].numel() else None)
+        del holder['bal']
+        return sf
+
+    def keep(self, chrom, holder, disp_idx, bias):
+        """Registers a prepared chromosome (its stage files just queued)."""
+        torch = self.torch
+        n = int(holder['row'].shape[0])
+        t_di = torch.from_numpy(np.ascontiguousarray(
+            disp_idx, dtype=np.uint8)).to(self.dev)
+        files = {self.h._npy(s, chrom): ('ours', self.h.write_generation(
+            self.h._npy(s, chrom))) for s in self.STAGES}
+        files.update(self._bias_stamps(chrom))
+        self.chroms[chrom] = ChromDev(
+            holder['row'], holder['col'], holder['raw'], holder['sf'],
+            holder['sf'].dim() == 1, t_di, int(np.count_nonzero(disp_idx)),
+            bias, files)
+        if self.session is not None and chrom in self.session['chroms']:
+            self.session = None
+        return n
+
+    # -- the chromosome's union, resident or from the outdir ------------
+    def chrom(self, chrom):
+        ent = self.chroms.get(chrom)
+        if ent is not None and self._current(ent.files):
+            return ent
+        self.chroms.pop(chrom, None)
+        return self._load(chrom)
+
+    def _load(self, chrom):
+        """The union of a chromosome another process (or an earlier object)
+        prepared: read from the outdir files and uploaded once."""
+        torch = self.torch
+        h = self.h
+        files = {}
+        arrs = {}
+        for s in self.STAGES:
+            fname = h._npy(s, chrom)
+            files[fname] = self._token(fname)
+            arrs[s] = h.load_data(s, chrom)
+        files.update(self._bias_stamps(chrom))
+        raw = np.asarray(arrs['raw'])
+        if raw.size and (raw.min() < 0 or raw.max() > np.iinfo(np.int32).max):
+            raise _native.H3DError('raw counts must be in [0, 2^31)')
+        sf = np.ascontiguousarray(arrs['size_factors'], dtype=np.float64)
+
+        def up(a, dt):
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(
+                self.dev)
+        di = np.asarray(arrs['disp_idx'], dtype=bool)
+        ent = ChromDev(up(arrs['row'], np.int32), up(arrs['col'], np.int32),
+                       up(raw, np.int32), up(sf, np.float64), sf.ndim == 1,
+                       up(di, np.uint8), int(np.count_nonzero(di)),
+                       h.load_bias(chrom), files)
+        self.chroms[chrom] = ent
+        return ent
+
+    # -- estimate_disp / lrt inputs ---------------------------------------
+    def disp_pixels(self, chroms, R):
+        """raw (n, R) int32, f (n, R), dist (n) of the disp pixels of
+        ``chroms`` concatenated in chromosome order (analysis.py:169-183),
+        on the device, and the offsets between the chromosomes."""
+        torch = self.torch
+        ents = [self.chrom(c) for c in chroms]
+        offsets = np.concatenate([[0], np.cumsum([e.n_disp for e in ents])])
+        n = int(offsets[-1])
+        t_raw = torch.empty((n, R), dtype=torch.int32, device=self.dev)
+        t_f = torch.empty((n, R), dtype=torch.float64, device=self.dev)
+        t_dist = torch.empty(n, dtype=torch.int32, device=self.dev)
+        for e, o in zip(ents, offsets[:-1]):
+            if not e.n:
+                continue
+            o = int(o)
+            self.ctx.disp_pixels_dev(
+                e.row.data_ptr(), e.col.data_ptr(), e.raw.data_ptr(),
+                e.sf.data_ptr(), e.sf_per_rep, e.bias, e.disp_idx.data_ptr(),
+                e.n, R, e.n_disp,
+                t_raw.data_ptr() + o * R * 4 if e.n_disp else None,
+                t_f.data_ptr() + o * R * 8 if e.n_disp else None,
+                t_dist.data_ptr() + o * 4 if e.n_disp else None)
+        return t_raw, t_f, t_dist, offsets
+
+    def start_session(self, chroms, t_raw, t_f, t_dist, offsets, t_tab, D, C):
+        """estimate_disp's resident result for lrt: its pixels and device
+        tables, valid while its disp files and its chromosomes' stage files
+        are current."""
+        files = {}
+        for c in chroms:
+            files[self.h._npy('disp', c)] = self._token(self.h._npy('disp', c))
+            files.update(self.chroms[c].files)
+        self.session = {'chroms': tuple(chroms), 'raw': t_raw, 'f': t_f,
+                        'dist': t_dist, 'offsets': offsets, 'tables': t_tab,
+                        'D': D, 'C': C, 'files': files}
+
+    def lrt_session(self, chroms):
+        """The session if it covers exactly ``chroms`` and is current."""
+        s = self.session
+        if s is None or s['chroms'] != tuple(chroms):
+            return None
+        if not self._current(s['files']):
+            self.session = None
+            return None
+        return s

@@ -253,13 +253,21 @@ struct GangTables {
   long long timeout = 0;
 };
 
-// next tag epoch of the gang exchange: the tags are cleared only when their
-// buffer is new or the epoch wraps (tag = epoch << 10 | evaluation + 1)
+// next tag epoch of the gang exchange: the tags are cleared when their
+// buffer is new -- another pointer, or the same pointer handed out again by
+// a grown allocation (scratch frees and reallocates: the grown tail would
+// hold stale device words), i.e. another (pointer, capacity) -- or the epoch
+// wraps (tag = epoch << 10 | evaluation + 1). The whole allocation is
+// cleared, so a later call with another layout (S, gmax) inside the same
+// allocation only ever finds zeros or tags of older epochs.
 int gang_next_epoch(h3d_ctx* ctx, const GangTables& g, int S) {
-  if (ctx->gang_tag_buf != (void*)g.tag || ctx->gang_epoch >= (1 << 20)) {
-    if (hipMemsetAsync(g.tag, 0, (size_t)2 * S * g.gmax * 4, ctx->stream) != hipSuccess)
-      return -1;
+  const size_t cap = ctx->bufs["gang_tag"].second;
+  if (ctx->gang_tag_buf != (void*)g.tag || ctx->gang_tag_cap != cap ||
+      ctx->gang_epoch >= (1 << 20)) {
+    const size_t bytes = std::max(cap, (size_t)2 * S * g.gmax * 4);
+    if (hipMemsetAsync(g.tag, 0, bytes, ctx->stream) != hipSuccess) return -1;
     ctx->gang_tag_buf = (void*)g.tag;
+    ctx->gang_tag_cap = cap;
     ctx->gang_epoch = 0;
   }
   return ++ctx->gang_epoch;
@@ -1000,7 +1008,11 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         rc = fail(H3D_EHIP, "disp round copies failed: %s", hipGetErrorString(hipGetLastError()));
         break;
       }
-      if (treq) {
+      // (speculatively only where the smoother is the device's, enqueued
+      // without a wait; the host smoother of D > kTableMaxD runs once, on
+      // the final result, below -- on an intermediate poll it would block
+      // and could reject a table that is not final)
+      if (treq && D <= kTableMaxD) {
         rc = h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac, treq->aff,
                                  treq->d_tables);
         if (rc) {
@@ -1135,7 +1147,15 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     all |= fl[sg];
   }
   if (seg_flags_out) std::memcpy(seg_flags_out, fl.data(), S * 4);
-  return flags_to_code(all);
+  if (const int frc = flags_to_code(all)) return frc;
+  if (have_res && treq && D > kTableMaxD) {
+    // the host smoother (h3d_disp_tables_dev's D > kTableMaxD branch), once,
+    // on the final result
+    const int trc = h3d_disp_tables_dev(ctx, d_res, D, C, treq->weighted, treq->frac,
+                                        treq->aff, treq->d_tables);
+    if (trc) return trc;
+  }
+  return 0;
 }
 }  // namespace
 

@@ -126,6 +126,7 @@ struct h3d_ctx {
   // launches) and the tag buffer it is valid for
   int gang_epoch = 0;
   void* gang_tag_buf = nullptr;
+  size_t gang_tag_cap = 0;  // the tag allocation's capacity when last cleared
   h3dint::TablePending tab_pending;
   // H3D_DEV_SEG_TABLES (default 1): estimate_disp's chunk / segment tables
   // built on the device (k_disp_tables) where no gangs are needed
@@ -137,6 +138,9 @@ struct h3d_ctx {
 namespace h3dint {
 
 constexpr int kLaunchBlock = 256;
+// distances per condition the device smoother holds in LDS (h3d_table.hip);
+// beyond it h3d_disp_tables_dev runs the host smoother inside the call
+constexpr int kTableMaxD = 1024;
 
 // grow-only device buffer of the ctx, by slot name (nullptr on OOM)
 void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes);

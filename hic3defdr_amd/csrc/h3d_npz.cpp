@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -72,12 +73,18 @@ int read_directory(FILE* f, std::vector<Member>* out) {
   if ((n_ent == 0xFFFF || cd_off == 0xFFFFFFFFu) && e >= 20 &&
       rd32(&t[e - 20]) == 0x07064b50u) {  // ZIP64 locator -> ZIP64 EOCD
     unsigned char z[56];
-    if (!read_at(f, rd64(&t[e - 20 + 8]), z, 56) || rd32(z) != 0x06064b50u)
+    const uint64_t z_off = rd64(&t[e - 20 + 8]);
+    if (z_off > size || size - z_off < 56 || !read_at(f, z_off, z, 56) ||
+        rd32(z) != 0x06064b50u)
       return fail(H3D_EARG, "npz: bad zip64 end record");
     n_ent = rd64(z + 32);
     cd_size = rd64(z + 40);
     cd_off = rd64(z + 48);
   }
+  // every size and offset read from the file is checked against the file
+  // before it sizes an allocation or a read
+  if (cd_off > size || cd_size > size - cd_off || n_ent > cd_size / 46)
+    return fail(H3D_EARG, "npz: central directory outside the file");
   std::vector<unsigned char> cd(cd_size);
   if (!read_at(f, cd_off, cd.data(), cd_size)) return fail(H3D_EARG, "npz: read failed");
   size_t p = 0;
@@ -90,6 +97,8 @@ int read_directory(FILE* f, std::vector<Member>* out) {
     m.csize = rd32(&cd[p + 20]);
     m.usize = rd32(&cd[p + 24]);
     const uint16_t nl = rd16(&cd[p + 28]), xl = rd16(&cd[p + 30]), cl = rd16(&cd[p + 32]);
+    if (p + 46 + (size_t)nl + xl + cl > cd.size())
+      return fail(H3D_EARG, "npz: central directory entry overruns the directory");
     m.local_off = rd32(&cd[p + 42]);
     m.name.assign((const char*)&cd[p + 46], nl);
     // ZIP64 extra field: the 0xFFFFFFFF fields follow in order
@@ -97,14 +106,21 @@ int read_directory(FILE* f, std::vector<Member>* out) {
     const size_t xe = x + xl;
     while (x + 4 <= xe) {
       const uint16_t id = rd16(&cd[x]), len = rd16(&cd[x + 2]);
+      if (x + 4 + len > xe) return fail(H3D_EARG, "npz: extra field overruns its entry");
       if (id == 0x0001) {
         size_t q = x + 4;
-        if (m.usize == 0xFFFFFFFFu) m.usize = rd64(&cd[q]), q += 8;
-        if (m.csize == 0xFFFFFFFFu) m.csize = rd64(&cd[q]), q += 8;
-        if (m.local_off == 0xFFFFFFFFu) m.local_off = rd64(&cd[q]);
+        const size_t qe = x + 4 + len;
+        if (m.usize == 0xFFFFFFFFu && q + 8 <= qe) m.usize = rd64(&cd[q]), q += 8;
+        if (m.csize == 0xFFFFFFFFu && q + 8 <= qe) m.csize = rd64(&cd[q]), q += 8;
+        if (m.local_off == 0xFFFFFFFFu && q + 8 <= qe) m.local_off = rd64(&cd[q]);
       }
       x += 4 + len;
     }
+    // a member lies inside the file, and deflate expands at most ~1032x
+    if (m.local_off > size || m.csize > size - m.local_off ||
+        (m.method == 0 && m.usize != m.csize) ||
+        m.usize > m.csize * 1040 + 4096)
+      return fail(H3D_EARG, "npz: member %s sizes outside the file", m.name.c_str());
     out->push_back(m);
     p += 46 + nl + xl + cl;
   }
@@ -332,9 +348,38 @@ int small_member(Archive& a, const char* name, std::vector<unsigned char>* bytes
 
 }  // namespace
 
+namespace {
+int csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t* nnz);
+int csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* indptr,
+             int32_t* indices, double* data, int* canonical);
+}  // namespace
+
 extern "C" {
 
+// the entry points turn any exception (a bad_alloc sized by a corrupt
+// archive) into an error code: nothing may unwind through the C ABI
 int h3d_npz_csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
+  try {
+    return csr_info(path, n_rows, n_cols, nnz);
+  } catch (const std::exception& e) {
+    return fail(H3D_ENOMEM, "npz: %s", e.what());
+  }
+}
+
+int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* indptr,
+                     int32_t* indices, double* data, int* canonical) {
+  try {
+    return csr_read(path, n_rows, nnz, indptr, indices, data, canonical);
+  } catch (const std::exception& e) {
+    return fail(H3D_ENOMEM, "npz: %s", e.what());
+  }
+}
+
+}  // extern "C"
+
+namespace {
+
+int csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
   if (!path || !n_rows || !n_cols || !nnz) return fail(H3D_EARG, "null argument");
   Archive a;
   if (int rc = open_archive(path, &a)) return rc;
@@ -358,6 +403,10 @@ int h3d_npz_csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t
   if (int rc = member_head(a.file.f, *md, 4096, &head)) return rc;
   Npy hd;
   if (int rc = parse_npy(head, &hd, "data.npy")) return rc;
+  if (shp[0] < 0 || shp[1] < 0 || shp[0] > ((int64_t)1 << 40))
+    return fail(H3D_EARG, "npz: bad shape");
+  for (int64_t v : hd.shape)
+    if (v < 0) return fail(H3D_EARG, "npz: bad data shape");
   *n_rows = shp[0];
   *n_cols = shp[1];
   *nnz = npy_count(hd);
@@ -367,10 +416,11 @@ int h3d_npz_csr_info(const char* path, int64_t* n_rows, int64_t* n_cols, int64_t
 // the three arrays into caller buffers (n_rows + 1, nnz, nnz); *canonical =
 // 1 when every row's column indices are strictly increasing (sorted, no
 // duplicates: what the union kernels take as is)
-int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* indptr,
-                     int32_t* indices, double* data, int* canonical) {
+int csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* indptr,
+             int32_t* indices, double* data, int* canonical) {
   if (!path || !indptr || (nnz && (!indices || !data)) || !canonical)
     return fail(H3D_EARG, "null argument");
+  if (n_rows < 0 || nnz < 0) return fail(H3D_EARG, "npz: n_rows / nnz");
   Archive a;
   if (int rc = open_archive(path, &a)) return rc;
   const char* names[3] = {"indptr.npy", "indices.npy", "data.npy"};
@@ -383,7 +433,9 @@ int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* ind
       errs[j] = h3derr::last();
       return;
     }
-    // each thread reads through its own FILE (one stream is not shareable)
+    // each thread reads through its own FILE (one stream is not shareable);
+    // an exception (bad_alloc) must not leave the thread
+    try {
     File own;
     own.f = fopen(path, "rb");
     std::vector<unsigned char> b;
@@ -403,6 +455,10 @@ int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* ind
     }
     rcs[j] = rc;
     if (rc) errs[j] = h3derr::last();
+    } catch (const std::exception& ex) {
+      rcs[j] = H3D_ENOMEM;
+      errs[j] = std::string("npz: ") + ex.what();
+    }
   };
   std::thread t1(work, 1), t2(work, 2);
   work(0);
@@ -411,9 +467,13 @@ int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* ind
   for (int j = 0; j < 3; ++j)
     if (rcs[j]) return fail(rcs[j], "%s", errs[j].c_str());
   if (indptr[0] != 0 || indptr[n_rows] != nnz) return fail(H3D_EARG, "npz: bad indptr");
+  // the whole indptr before any row is scanned: 0 <= indptr[r] <=
+  // indptr[r + 1] <= nnz, so no row reads past the indices
+  for (int64_t r = 0; r < n_rows; ++r)
+    if (indptr[r + 1] < indptr[r] || indptr[r + 1] > nnz)
+      return fail(H3D_EARG, "npz: bad indptr (row %lld)", (long long)r);
   int canon = 1;
   for (int64_t r = 0; r < n_rows && canon; ++r) {
-    if (indptr[r + 1] < indptr[r]) return fail(H3D_EARG, "npz: bad indptr");
     for (int64_t k = indptr[r] + 1; k < indptr[r + 1]; ++k)
       if (indices[k] <= indices[k - 1]) {
         canon = 0;
@@ -424,4 +484,4 @@ int h3d_npz_csr_read(const char* path, int64_t n_rows, int64_t nnz, int64_t* ind
   return 0;
 }
 
-}  // extern "C"
+}  // namespace

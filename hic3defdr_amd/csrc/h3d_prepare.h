@@ -355,4 +355,49 @@ static __global__ void k_minus_one(int32_t* __restrict__ v, int64_t n) {
     v[k] -= 1;
 }
 
+// ---- the disp pixels of a chromosome (estimate_disp / lrt inputs) ----------
+
+// The disp_idx pixels of one chromosome, compacted in pixel order: raw, dist
+// = col - row and f = bias[row] * bias[col] * sf -- the reference's products
+// in its order (analysis.py:174-183 and :272-275, numpy evaluates left to
+// right; a product of three never contracts, so the bits are numpy's). sel
+// = the selected union-pixel indices (DeviceSelect over disp_idx). sf is
+// (N, R), or (R,) with sf_per_rep (the non-conditional norms). Rows of R <= 4
+// int32 / f64 go out as whole 16 B words where aligned.
+static __global__ void k_disp_pixels(const int32_t* __restrict__ sel, int64_t n_out,
+                                     const int32_t* __restrict__ row,
+                                     const int32_t* __restrict__ col,
+                                     const int32_t* __restrict__ raw,
+                                     const double* __restrict__ sf, int sf_per_rep,
+                                     const double* __restrict__ bias, int R,
+                                     int32_t* __restrict__ raw_out,
+                                     double* __restrict__ f_out,
+                                     int32_t* __restrict__ dist_out) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_out;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = sel[j];
+    const int64_t r0 = row[i], c0 = col[i];
+    dist_out[j] = (int32_t)(c0 - r0);
+    for (int k = 0; k < R; ++k) {
+      raw_out[j * R + k] = raw[i * R + k];
+      const double bb = bias[r0 * R + k] * bias[c0 * R + k];
+      f_out[j * R + k] = bb * (sf_per_rep ? sf[k] : sf[i * R + k]);
+    }
+  }
+}
+
+// disp[i, c] = table[dist[i], c] (analysis.py:218 disp_fn(dist): the fitted
+// function evaluated at integer distances IS its tabulation); NaN outside
+// [0, D)
+static __global__ void k_table_gather(const double* __restrict__ table, int D, int C,
+                                      const int32_t* __restrict__ dist, int64_t n,
+                                      double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = dist[i];
+    const bool in = d >= 0 && d < D;
+    for (int c = 0; c < C; ++c) out[i * C + c] = in ? table[(int64_t)d * C + c] : NAN;
+  }
+}
+
 }  // namespace h3d

@@ -158,6 +158,13 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
 
 int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
                    double* balanced, int64_t n_px) {
+  return h3d_union_fill_dev(ctx, row, col, raw, balanced, n_px, nullptr, nullptr, nullptr,
+                            nullptr);
+}
+
+int h3d_union_fill_dev(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
+                       double* balanced, int64_t n_px, int32_t* d_row_out,
+                       int32_t* d_col_out, int32_t* d_raw_out, double* d_bal_out) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   PrepUnion& P = ctx->prep;
   if (n_px != P.n_px) return fail(H3D_EARG, "n_px %lld != counted %lld", (long long)n_px, (long long)P.n_px);
@@ -171,51 +178,165 @@ int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
   int64_t* d_raw = (int64_t*)scratch(ctx, "u_out_raw", n_px * R * 8);
   double* d_bal = (double*)scratch(ctx, "u_out_bal", n_px * R * 8);
   int32_t* keep = (int32_t*)scratch(ctx, "u_keep", std::max<int64_t>(P.n_runs, 1) * 4);
-  if (!d_row || !d_col || !d_raw || !d_bal) return fail(H3D_ENOMEM, "union out");
+  int* d_ovf = (int*)scratch(ctx, "ovf", 4);
+  if (!d_row || !d_col || !d_raw || !d_bal || !d_ovf) return fail(H3D_ENOMEM, "union out");
   hipLaunchKernelGGL(k_union_fill, dim3(grid_for(ctx, P.n_runs)), dim3(kBlock), 0, s,
                      P.keys_sorted, P.ent_sorted, P.run_start, keep, P.px_of_run,
                      P.n_runs, P.n_entries, P.ent_rep, P.ent_val, R, P.n_bins, P.bias,
                      d_row, d_col, d_raw, d_bal);
+  // the caller's device copies (the product's resident chromosome): the
+  // counts as int32, the width every disp / lrt kernel reads
+  if (d_row_out) HIP_TRY(hipMemcpyAsync(d_row_out, d_row, n_px * 4, hipMemcpyDeviceToDevice, s));
+  if (d_col_out) HIP_TRY(hipMemcpyAsync(d_col_out, d_col, n_px * 4, hipMemcpyDeviceToDevice, s));
+  if (d_bal_out)
+    HIP_TRY(hipMemcpyAsync(d_bal_out, d_bal, n_px * R * 8, hipMemcpyDeviceToDevice, s));
+  int ovf = 0;
+  if (d_raw_out) {
+    HIP_TRY(hipMemsetAsync(d_ovf, 0, 4, s));
+    hipLaunchKernelGGL(k_i64_to_i32, dim3(grid_for(ctx, n_px * R)), dim3(kBlock), 0, s, d_raw,
+                       d_raw_out, n_px * R, d_ovf);
+    HIP_TRY(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipMemcpyAsync(row, d_row, n_px * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(col, d_col, n_px * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(raw, d_raw, n_px * R * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(balanced, d_bal, n_px * R * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (ovf) return fail(H3D_EINPUT, "raw counts must be in [0, 2^31) for the device copy");
   return 0;
 }
 
+// d_disp_idx (n) 0/1 -> the chromosome's disp pixels (k_disp_pixels)
+int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col,
+                        const int32_t* d_raw, const double* d_sf, int sf_per_rep,
+                        const double* bias, int n_bins, const uint8_t* d_disp_idx,
+                        int64_t n, int R, int64_t n_disp, int32_t* d_raw_out,
+                        double* d_f_out, int32_t* d_dist_out) {
+  if (!ctx || !bias) return fail(H3D_EARG, "null argument");
+  if (R < 1 || R > kMaxReps || n_bins < 1 || n < 0 || n_disp < 0 || n_disp > n)
+    return fail(H3D_EARG, "R=%d n_bins=%d n=%lld n_disp=%lld", R, n_bins, (long long)n,
+                (long long)n_disp);
+  if (n >= ((int64_t)1 << 31)) return fail(H3D_EARG, "n=%lld exceeds 2^31", (long long)n);
+  if (n == 0) return 0;
+  if (!d_row || !d_col || !d_raw || !d_sf || !d_disp_idx)
+    return fail(H3D_EARG, "null device input");
+  if (n_disp > 0 && (!d_raw_out || !d_f_out || !d_dist_out))
+    return fail(H3D_EARG, "null device output");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  int32_t* d_sel = (int32_t*)scratch(ctx, "dp_sel", (size_t)std::max<int64_t>(n, 1) * 4);
+  int32_t* d_cnt = (int32_t*)scratch(ctx, "dp_cnt", 4);
+  double* d_bias = (double*)scratch(ctx, "dp_bias", (size_t)n_bins * R * 8);
+  if (!d_sel || !d_cnt || !d_bias) return fail(H3D_ENOMEM, "disp pixel scratch");
+  HIP_TRY(hipMemcpyAsync(d_bias, bias, (size_t)n_bins * R * 8, hipMemcpyHostToDevice, s));
+  hipcub::CountingInputIterator<int32_t> it(0);
+  size_t tb = 0;
+  HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, d_disp_idx, d_sel, d_cnt, (int)n, s));
+  void* tmp = scratch(ctx, "cub_tmp_sel", tb);
+  if (!tmp) return fail(H3D_ENOMEM, "select temp");
+  HIP_TRY(hipcub::DeviceSelect::Flagged(tmp, tb, it, d_disp_idx, d_sel, d_cnt, (int)n, s));
+  int32_t cnt = 0;
+  HIP_TRY(hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (cnt != n_disp)
+    return fail(H3D_EARG, "disp_idx selects %d pixels, caller expects %lld", cnt,
+                (long long)n_disp);
+  if (n_disp == 0) return 0;
+  hipLaunchKernelGGL(k_disp_pixels, dim3(grid_for(ctx, n_disp)), dim3(kBlock), 0, s, d_sel,
+                     n_disp, d_row, d_col, d_raw, d_sf, sf_per_rep, d_bias, R, d_raw_out,
+                     d_f_out, d_dist_out);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int h3d_table_gather_dev(h3d_ctx* ctx, const double* d_tables, int D, int C,
+                         const int32_t* d_dist, int64_t n, double* d_out) {
+  if (!ctx || !d_tables || D < 1 || C < 1 || C > kMaxConds || n < 0)
+    return fail(H3D_EARG, "null argument / D / C / n");
+  // a pending device smoother is settled first (a degenerate fit is redone
+  // on the host into the same buffer)
+  if (int rc = h3d_disp_tables_wait(ctx)) return rc;
+  if (n == 0) return 0;
+  if (!d_dist || !d_out) return fail(H3D_EARG, "null device buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_table_gather, dim3(grid_for(ctx, n)), dim3(kBlock), 0, ctx->stream,
+                     d_tables, D, C, d_dist, n, d_out);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+namespace {
+int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_balanced,
+                      const int32_t* dist, int64_t n, int R, int norm, int n_bins,
+                      double* sf_out, double* d_sf_out);
+}  // namespace
+
 int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
                      int64_t n, int R, int norm, int n_bins, double* sf_out) {
-  if (!ctx || (n > 0 && !balanced) || !sf_out) return fail(H3D_EARG, "null argument");
+  return size_factors_impl(ctx, balanced, nullptr, dist, n, R, norm, n_bins, sf_out,
+                           nullptr);
+}
+
+int h3d_size_factors_dev(h3d_ctx* ctx, const double* d_balanced, const int32_t* dist,
+                         int64_t n, int R, int norm, int n_bins, double* sf_out,
+                         double* d_sf_out) {
+  if (n > 0 && !d_balanced) return fail(H3D_EARG, "null device balanced");
+  return size_factors_impl(ctx, nullptr, d_balanced, dist, n, R, norm, n_bins, sf_out,
+                           d_sf_out);
+}
+
+}  // extern "C"
+
+namespace {
+int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_balanced,
+                      const int32_t* dist, int64_t n, int R, int norm, int n_bins,
+                      double* sf_out, double* d_sf_out) {
+  if (!ctx || (n > 0 && !balanced && !d_balanced) || !sf_out)
+    return fail(H3D_EARG, "null argument");
   if (R < 1 || R > kMaxReps || n_bins < 0) return fail(H3D_EARG, "R=%d n_bins=%d", R, n_bins);
   if (norm < H3D_NORM_CONDITIONAL_MOR || norm > H3D_NORM_NO_SCALING)
     return fail(H3D_EARG, "norm %d", norm);
   const bool conditional =
       norm == H3D_NORM_CONDITIONAL_MOR || norm == H3D_NORM_CONDITIONAL_SCALING;
   const bool mor = norm == H3D_NORM_CONDITIONAL_MOR || norm == H3D_NORM_MEDIAN_OF_RATIOS;
+  // the (R,) factors of the global norms into the caller's device copy too
+  auto global_out = [&]() -> int {
+    if (d_sf_out) {
+      HIP_TRY(hipSetDevice(ctx->device));
+      HIP_TRY(hipMemcpyAsync(d_sf_out, sf_out, R * 8, hipMemcpyHostToDevice, ctx->stream));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    return 0;
+  };
   if (norm == H3D_NORM_NO_SCALING) {  // scaling.py:24: ones(R), no data pass
     for (int r = 0; r < R; ++r) sf_out[r] = 1.0;
-    return 0;
+    return global_out();
   }
   if (conditional && n > 0 && !dist) return fail(H3D_EARG, "null dist");
   if (n == 0) {
-    if (!conditional)
+    if (!conditional) {
       for (int r = 0; r < R; ++r) sf_out[r] = NAN;  // median / sums of nothing
+      return global_out();
+    }
     return 0;
   }
   if (n >= ((int64_t)1 << 31) / R) return fail(H3D_EARG, "n too large");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  double* d_bal = (double*)scratch(ctx, "sf_bal", n * R * 8);
+  double* d_bal = d_balanced ? nullptr : (double*)scratch(ctx, "sf_bal", n * R * 8);
   int32_t* d_dist = (int32_t*)scratch(ctx, "sf_dist", n * 4);
   int32_t* d_dist_s = (int32_t*)scratch(ctx, "sf_dist_s", n * 4);
   int32_t* d_idx = (int32_t*)scratch(ctx, "sf_idx", n * 4);
   int32_t* d_perm = (int32_t*)scratch(ctx, "sf_perm", n * 4);
   int32_t* d_bin = (int32_t*)scratch(ctx, "sf_bin", n * 4);
   double* d_sf = (double*)scratch(ctx, "sf_out", n * R * 8);
-  if (!d_bal || !d_dist || !d_dist_s || !d_idx || !d_perm || !d_bin || !d_sf)
+  if ((!d_balanced && !d_bal) || !d_dist || !d_dist_s || !d_idx || !d_perm || !d_bin || !d_sf)
     return fail(H3D_ENOMEM, "size factor scratch");
-  HIP_TRY(hipMemcpyAsync(d_bal, balanced, n * R * 8, hipMemcpyHostToDevice, s));
+  if (!d_balanced)
+    HIP_TRY(hipMemcpyAsync(d_bal, balanced, n * R * 8, hipMemcpyHostToDevice, s));
+  const double* bal = d_balanced ? d_balanced : d_bal;
   hipLaunchKernelGGL(k_iota, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_idx, n);
   size_t tb = 0;
   void* tmp = nullptr;
@@ -278,7 +399,7 @@ int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
     if (!d_valid || !d_keys || !d_keys_s || !d_segb || !d_sege)
       return fail(H3D_ENOMEM, "median scratch");
     HIP_TRY(hipMemsetAsync(d_valid, 0, (size_t)nb * 4, s));
-    hipLaunchKernelGGL(k_mor_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bal,
+    hipLaunchKernelGGL(k_mor_keys, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, bal,
                        d_perm, n, R, d_bin, d_keys, d_valid);
     std::vector<int64_t> segb((size_t)nb * R), sege((size_t)nb * R);
     for (int r = 0; r < R; ++r)
@@ -326,7 +447,7 @@ int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, d_bin_orig, d_bin_orig_s, d_iota,
                                                  members, (int)n, 0, end_bit, s));
     }
-    hipLaunchKernelGGL(k_bin_colsum, dim3((nb * R + 255) / 256), dim3(256), 0, s, d_bal,
+    hipLaunchKernelGGL(k_bin_colsum, dim3((nb * R + 255) / 256), dim3(256), 0, s, bal,
                        members, d_bstart, nb, R, d_spb);
     std::vector<double> colsum((size_t)nb * R);
     HIP_TRY(hipMemcpyAsync(colsum.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost,
@@ -342,7 +463,7 @@ int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
   }
   if (!conditional) {
     std::memcpy(sf_out, spb.data(), R * 8);
-    return 0;
+    return global_out();
   }
   // 3. per-pixel factors (scaling.py:88-105)
   if (n_bins > 0) {
@@ -372,10 +493,14 @@ int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
     hipLaunchKernelGGL(k_sf_exact, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_perm,
                        d_bin, n, R, d_spb, d_sf);
   }
+  if (d_sf_out) HIP_TRY(hipMemcpyAsync(d_sf_out, d_sf, n * R * 8, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(sf_out, d_sf, n * R * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
                           const int32_t* dist, int64_t n, int R, int n_bins,

@@ -51,7 +51,7 @@ namespace h3dtab {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kMaxD = 1024;  // distances per table held in LDS
+constexpr int kMaxD = h3dint::kTableMaxD;  // distances per table held in LDS
 constexpr int kRobustIters = 3;
 constexpr int kRollWindow = 20;
 constexpr int kStamps = 16;

@@ -40,9 +40,14 @@ def qcml(data, f=None, max_iter=10, tol=1e-4):
 def qcml_batch(segments, max_iter=10, tol=1e-4):
     """qcml over many segments in ONE estimate_disp driver call: ``segments``
     is a list of (data, f) pairs as qcml takes them (f may be None); returns
-    the list of dispersions, each equal to qcml(data, f) bit for bit (every
-    segment's equalize / Brent search runs on its own pixels, in their own
-    order). The reference's estimate_disp calls qcml once per (distance,
+    the list of dispersions, each the qcml of its own pixels -- equal to
+    qcml(data, f) up to the summation order of the NLL, which depends on the
+    whole call (the gang slice size follows the call's pixel count, and one
+    workgroup per segment or gangs are chosen by the live-segment count), so
+    a segment can land elsewhere inside Brent's tolerance (xatol 1e-5 in
+    delta = disp / (1 + disp)), as the reference itself does under a pixel
+    permutation (tests/golden/cfg2_spread.npz). The reference's
+    estimate_disp calls qcml once per (distance,
     condition) (analysis.py:198-246 -> dispersion.py:10-43): a caller
     patching that loop gathers its segments first and makes this one call
     instead of several hundred single-segment driver runs."""

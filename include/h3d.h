@@ -118,6 +118,15 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins, const int64_t* const* indpt
  * raw / (bias[row, r] * bias[col, r]) (analysis.py:91-101). */
 int h3d_union_fill(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
                    double* balanced, int64_t n_px);
+/* h3d_union_fill that also leaves the union in caller-owned DEVICE buffers
+ * (each may be NULL): d_row / d_col (n_px) int32, d_raw (n_px, R) int32 --
+ * H3D_EINPUT, after the host outputs are written, if a count does not fit
+ * --, d_balanced (n_px, R). The product keeps a chromosome resident this way
+ * between prepare_data and estimate_disp / lrt (analysis.py:128-133 writes
+ * the same arrays to the outdir, :169-183 and :261-275 read them back). */
+int h3d_union_fill_dev(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
+                       double* balanced, int64_t n_px, int32_t* d_row,
+                       int32_t* d_col, int32_t* d_raw, double* d_balanced);
 
 /* Distance-conditional median-of-ratios size factors (scaling.py:68-127) with
  * n_bins equal-number distance bins (stable tie order), or
@@ -133,6 +142,27 @@ int h3d_size_factors_cmor(h3d_ctx* ctx, const double* balanced,
  * global methods, may be NULL). */
 int h3d_size_factors(h3d_ctx* ctx, const double* balanced, const int32_t* dist,
                      int64_t n, int R, int norm, int n_bins, double* sf_out);
+/* The same on a DEVICE balanced (n, R) (h3d_union_fill_dev's), dist (n) on
+ * the host; sf on the host as h3d_size_factors writes it and, when d_sf_out
+ * is not NULL, in that device buffer too ((n, R) or (R,)). */
+int h3d_size_factors_dev(h3d_ctx* ctx, const double* d_balanced,
+                         const int32_t* dist, int64_t n, int R, int norm,
+                         int n_bins, double* sf_out, double* d_sf_out);
+
+/* The disp pixels of one chromosome on the device (analysis.py:169-183 for
+ * estimate_disp, :261-275 for lrt): the union pixels whose d_disp_idx (n,
+ * 0/1) is set, in pixel order -> d_raw_out (n_disp, R) int32, d_f_out
+ * (n_disp, R) = bias[row] * bias[col] * sf (numpy's products in numpy's
+ * order), d_dist_out (n_disp) = col - row. Inputs: d_row / d_col (n),
+ * d_raw (n, R) int32, d_sf (n, R), or (R,) with sf_per_rep (the
+ * non-conditional norms, broadcast as analysis.py:274-275 does), bias
+ * (n_bins, R) on the HOST (core.py:35-60, filtered). n_disp = the caller's
+ * count of set flags (H3D_EARG if the device counts another). Synchronous. */
+int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col,
+                        const int32_t* d_raw, const double* d_sf, int sf_per_rep,
+                        const double* bias, int n_bins, const uint8_t* d_disp_idx,
+                        int64_t n, int R, int64_t n_disp, int32_t* d_raw_out,
+                        double* d_f_out, int32_t* d_dist_out);
 
 /* ---- estimate_disp ----------------------------------------------------- */
 
@@ -192,6 +222,14 @@ int h3d_estimate_disp_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                           double frac, double auto_frac_factor,
                           double* disp_per_dist, int32_t* seg_flags,
                           double* d_tables_out);
+
+/* disp[i, c] = tables[dist[i], c] on the device (analysis.py:218 disp_fn(dist)
+ * at integer distances = the tabulation; NaN outside [0, D)): d_tables (D,
+ * C), d_dist (n) -> d_disp_out (n, C). A pending h3d_disp_tables_dev /
+ * h3d_estimate_disp_dev table is settled first (h3d_disp_tables_wait).
+ * Synchronous. */
+int h3d_table_gather_dev(h3d_ctx* ctx, const double* d_tables, int D, int C,
+                         const int32_t* d_dist, int64_t n, double* d_disp_out);
 
 /* ---- lrt --------------------------------------------------------------- */
 

@@ -667,6 +667,100 @@ def run_full_cfg2(bins=20000, dmax=250, seed=0, chunk=20000, n_sample=50000):
           {k: len(v) for k, v in out.items() if k.startswith('calls_')})
 
 
+class _PermutedQcml(object):
+    """qcml (dispersion.py:10-43) on the segment's pixels in a seeded
+    permutation of their order. The result should not depend on the order
+    (the NLL is a sum over pixels), so this measures how far the reference
+    itself moves under a summation-order perturbation (np.sum's pairwise tree
+    over another order, dispersion.py:74-75). k = 0: the identity."""
+
+    def __init__(self, k):
+        self.k = k
+        self.qcml = dispersion.__dict__['_orig_qcml']
+
+    def __call__(self, data, f=None, **kw):
+        if self.k:
+            rng = np.random.default_rng([self.k, data.shape[0],
+                                         int(data.sum())])
+            perm = rng.permutation(data.shape[0])
+            data, f = data[perm], f[perm]
+        return self.qcml(data, f=f, **kw)
+
+
+def run_cfg2_spread(bins=20000, dmax=250, seed=0, perms=(0, 1, 2, 3, 4, 5),
+                    chunk=20000):
+    """The reference's own spread on the headline chromosome (bench.py cfg2,
+    the full_cfg2.npz workload): the reference's prepare_data once, then its
+    estimate_disp (analysis.py:135-223) once per pixel-order permutation of
+    every (distance, condition) segment (_PermutedQcml; k = 0 unpermuted),
+    its lrt (util/lrt.py:7-50) over all disp pixels in chunks (as
+    run_full_cfg2) and its bh() (analysis.py:286-303) with each run's disp.
+    cfg2_spread.npz: per permutation disp_per_dist, p / q on full_cfg2's
+    sample and top pixels, the call sets at q < 0.01 / 0.05 / 0.1."""
+    import multiprocessing
+    g = np.load(os.path.join(HERE, 'full_cfg2.npz'))
+    base = os.path.join('/tmp', 'h3golden_cfg2_data')
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, {'chrB0': bins}, dist_thresh_max=dmax,
+                                 seed=seed)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_cfg2_spread_out')
+    shutil.rmtree(outdir, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax)
+    h.prepare_data(n_threads=-1, verbose=False)
+    chrom = kw['chroms'][0]
+    bias = h.load_bias(chrom)
+    sf = h.load_data('size_factors', chrom)
+    di = h.load_data('disp_idx', chrom)
+    row = h.load_data('row', chrom, idx=di)
+    col = h.load_data('col', chrom, idx=di)
+    raw = h.load_data('raw', chrom, idx=di)
+    f = bias[row] * bias[col] * sf[di, :]
+    dsg = design.values
+    s, t = g['sample_idx'], g['top_idx']
+    dispersion.__dict__.setdefault('_orig_qcml', dispersion.qcml)
+    out = {'perms': np.array(perms), 'meta_bins': np.array(bins),
+           'meta_dmax': np.array(dmax), 'meta_seed': np.array(seed),
+           'meta_lrt_chunk': np.array(chunk)}
+    n = len(raw)
+    bounds = list(range(0, n, chunk)) + [n]
+    for k in perms:
+        dispersion.qcml = _PermutedQcml(k)
+        h.estimate_disp(n_threads=-1)
+        dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
+        dw = np.dot(h.load_data('disp', chrom), dsg.T)
+        tasks = [(raw[a:b], f[a:b], dw[a:b], dsg)
+                 for a, b in zip(bounds[:-1], bounds[1:])]
+        with multiprocessing.get_context('fork').Pool(8) as pool:
+            res = pool.map(_ref_lrt_chunk, tasks, chunksize=1)
+        p = np.concatenate([r[0] for r in res])
+        h.save_data(p, 'pvalues', chrom)
+        h.bh()
+        q = h.load_data('qvalues', chrom)
+        out['disp_per_dist__%d' % k] = dpd
+        out['p_sample__%d' % k] = p[s]
+        out['p_top__%d' % k] = p[t]
+        out['q_sample__%d' % k] = q[s]
+        out['q_top__%d' % k] = q[t]
+        for fdr in (0.01, 0.05, 0.1):
+            out['calls_%g__%d' % (fdr, k)] = np.where(q < fdr)[0].astype(
+                np.int32)
+        fin = np.isfinite(dpd)
+        rel = np.abs(dpd[fin] - g['disp_per_dist'][fin]) / \
+            g['disp_per_dist'][fin]
+        print('perm %d: segments > 1e-6 rel vs full_cfg2: %d, max rel %.3g; '
+              'sample p max rel %.3g, q max rel %.3g; calls %s' % (
+                  k, int(np.sum(rel > 1e-6)), rel.max(),
+                  np.max(np.abs(p[s] - g['p']) / g['p']),
+                  np.max(np.abs(q[s] - g['q']) / g['q']),
+                  [int(np.sum(q < fdr)) for fdr in (0.01, 0.05, 0.1)]),
+              flush=True)
+    dispersion.qcml = dispersion.__dict__['_orig_qcml']
+    np.savez_compressed(os.path.join(HERE, 'cfg2_spread.npz'), **out)
+
+
 SIM_EVALS = [(None, None, False), (None, 15, False), (16, 30, True),
              (31, None, False)]
 
@@ -772,6 +866,8 @@ if __name__ == '__main__':
         run_hard_cfg2()
     if 'full_cfg2' in which:
         run_full_cfg2()
+    if 'cfg2_spread' in which:
+        run_cfg2_spread()
     if 'sim' in which:
         run_sim()
     if 'alt' in which:

@@ -1,6 +1,7 @@
-"""The outdir write-through cache of save_data / load_data (CPU only): a
+"""The outdir write-behind cache of save_data / load_data (CPU only): a
 stage reading its own output back gets the saved values, fresh arrays every
-time, and any change of the file on disk wins over the cache."""
+time, queued writes land in order (flush(), interpreter exit), and once a
+write has landed any change of the file on disk wins over the cache."""
 import os
 import tempfile
 import time
@@ -40,10 +41,14 @@ def test_file_changed_on_disk_wins():
     h = _h()
     h.save_data(np.zeros(5), 'disp_idx', 'chr1')
     fname = os.path.join(h.outdir, 'disp_idx_chr1.npy')
+    h.flush()                            # the queued write has landed
+    assert h.is_current(fname)
     time.sleep(0.01)
     np.save(fname, np.ones(7))           # replaced behind the object's back
+    assert not h.is_current(fname)
     np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'), np.ones(7))
     h.save_data(np.zeros(5), 'disp_idx', 'chr1')   # cached again
+    h.flush()
     os.remove(fname)
     np.save(fname, np.full(5, 2.0))      # new inode, same size
     np.testing.assert_array_equal(h.load_data('disp_idx', 'chr1'),
@@ -54,6 +59,7 @@ def test_same_size_rewrite_in_place_with_mtime_restored():
     h = _h()
     h.save_data(np.zeros(5), 'disp_idx', 'chr1')
     fname = os.path.join(h.outdir, 'disp_idx_chr1.npy')
+    h.flush()
     st = os.stat(fname)
     time.sleep(0.02)                     # past the clock tick of the ctime
     with open(fname, 'r+b') as fh:       # same inode, same size
@@ -71,6 +77,7 @@ def test_cache_is_bounded_lru(monkeypatch):
     h = _h()
     for i in range(10):                  # 10 chromosomes' worth of stages
         h.save_data(np.full(100, float(i)), 'pvalues', 'chr%d' % i)
+        h.flush()
         assert h.cache_nbytes() <= 3 * 800
     assert h.cache_nbytes() == 3 * 800
     for i in range(10):                  # evicted ones come from disk
@@ -79,6 +86,7 @@ def test_cache_is_bounded_lru(monkeypatch):
     monkeypatch.setattr(CoreHiC3DeFDR, '_CACHE_BYTES', 0)
     h2 = _h()
     h2.save_data(np.zeros(10), 'pvalues', 'chr1')
+    h2.flush()
     assert h2.cache_nbytes() == 0
 
 
@@ -93,3 +101,33 @@ def test_all_chroms_with_offsets_and_idx():
     idx = x % 3 == 0
     got, offsets = h.load_data('pvalues', 'all', idx=idx)
     np.testing.assert_array_equal(got, x[idx])
+
+
+def test_write_behind_queue(monkeypatch):
+    """A queued array is served before its write lands, a reader of the file
+    waits for it, writes of one file land in order, and the queued array
+    cannot be changed under the writer."""
+    import threading
+    from hic3defdr_amd.analysis import core
+    gate = threading.Event()
+    real = core._write_npy
+
+    def slow(fname, data):
+        gate.wait(10)
+        return real(fname, data)
+    monkeypatch.setattr(core, '_write_npy', slow)
+    h = _h()
+    fname = os.path.join(h.outdir, 'pvalues_chr1.npy')
+    h.save_data(np.zeros(4), 'pvalues', 'chr1')
+    h.save_data(np.ones(4), 'pvalues', 'chr1')     # the later write wins
+    assert not os.path.exists(fname)
+    assert h.is_current(fname)
+    np.testing.assert_array_equal(h.load_data('pvalues', 'chr1'), np.ones(4))
+    gate.set()
+    np.testing.assert_array_equal(h.load_npy_file(fname), np.ones(4))
+    h.flush()
+    np.testing.assert_array_equal(np.load(fname), np.ones(4))
+    mine = np.arange(3.0)
+    h._save_npy(os.path.join(h.outdir, 'llr_chr1.npy'), mine, owned=True)
+    assert not mine.flags.writeable
+    h.flush()

@@ -7,7 +7,9 @@ chromosome of 20k bins, R = 4, dist_thresh_max 250) on the GPU:
   tests/golden/make_golden.py run_hard_cfg2);
 - the whole chromosome through the product's run_to_qvalues is held to the
   reference's own run on it (tests/golden/full_cfg2.npz: disp_per_dist,
-  sampled p / q, the smallest p-values, identical call sets);
+  sampled p / q, the smallest p-values, identical call sets) and to the
+  reference's own results under six pixel orders of its input
+  (tests/golden/cfg2_spread.npz);
 - and to size-independent properties: no status flags, p in [0, 1], no NaN
   outside empty segments, and bit-identical results on a second call.
 """
@@ -79,41 +81,65 @@ def _delta(disp):
     return disp / (1.0 + disp)
 
 
+def _reference_orders():
+    """The reference's own results on the cfg2 chromosome under six pixel
+    orders of every (distance, condition) segment (tests/golden/
+    cfg2_spread.npz, make_golden.py run_cfg2_spread; order 0 = the
+    reference's, = full_cfg2.npz): disp_per_dist, p / q on full_cfg2's
+    sample and top pixels."""
+    sp = golden('cfg2_spread.npz')
+    return [{key: sp['%s__%d' % (key, k)] for key in (
+        'disp_per_dist', 'p_sample', 'p_top', 'q_sample', 'q_top',
+        'calls_0.01', 'calls_0.05', 'calls_0.1')} for k in sp['perms']]
+
+
+def rel_err_arr(a, b):
+    return np.abs(a - b) / np.abs(b)
+
+
 def test_cfg2_full_size_vs_reference(ctx, cfg2):
     """The whole headline chromosome (3.76 M disp pixels) against the
     reference's own prepare_data + estimate_disp + (chunked) lrt + bh on it
-    (tests/golden/full_cfg2.npz, make_golden.py run_full_cfg2).
+    (tests/golden/full_cfg2.npz, make_golden.py run_full_cfg2) and against
+    the reference's own results under other pixel orders of its input
+    (cfg2_spread.npz, see test_reference_order_spread_fixture).
 
-    estimate_disp: the 502 (distance, condition) bounded-Brent searches
+    estimate_disp: the 494 (distance, condition) bounded-Brent searches
     (scipy xatol 1e-5 in delta = disp / (1 + disp)) follow the reference's
     trial points only while every comparison of two NLL values goes the same
-    way; NLL sums over ~15 k pixels that differ in the last bits (another
-    summation order, other lgamma / log implementations) can flip a
-    near-tied comparison, after which that search ends at another point
-    inside its tolerance. So: >= 99 % of the segments <= 1e-6 relative,
-    every segment within 2 xatol in delta.
+    way; NLL sums that differ in the last bits (another summation order,
+    other lgamma / log implementations) can flip a near-tied comparison --
+    the reference's own sums do under a pixel permutation. Bars: every
+    segment within 1e-6 of the reference under one of its six orders except
+    at most one, and that one within xatol in delta.
 
     lrt + bh, stage-isolated at full size: the product's smoother + LRT + BH
     on the reference's disp_per_dist -> p / q <= 1e-6 on the seeded sample
     and on the 2,000 smallest p-values, identical call sets.
 
-    End to end (the product's own disp_per_dist): identical call sets at
-    q < 0.01 / 0.05 / 0.1, p / q on the sample within 1e-3 relative (the
-    smoothed table moves by what a tolerance-level segment moves it)."""
+    End to end (the product's own disp_per_dist): p / q on the sample and
+    the top pixels within 1e-6 of the reference's end-to-end result under
+    one of its six pixel orders (the measured device values: 1e-9 to 3e-7,
+    r04a), identical call sets at q < 0.01 / 0.05 / 0.1."""
     from hic3defdr_amd import _native
     g = golden('full_cfg2.npz')
+    orders = _reference_orders()
     raw, f, dist, design, out = cfg2
     assert len(out['pvalues']) == int(g['n_disp_pixels'])
     dpd, ref = out['disp_per_dist'], g['disp_per_dist']
     np.testing.assert_array_equal(np.isnan(dpd), np.isnan(ref))
     fin = np.isfinite(ref)
-    rel = np.abs(dpd[fin] - ref[fin]) / ref[fin]
-    print('disp_per_dist: %d segments, %d > 1e-6 rel, max rel %.3g, max '
-          '|d delta| %.3g' % (rel.size, int(np.sum(rel > 1e-6)), rel.max(),
-                             np.max(np.abs(_delta(dpd[fin]) -
-                                           _delta(ref[fin])))))
-    assert np.mean(rel <= 1e-6) >= 0.99
-    assert np.max(np.abs(_delta(dpd[fin]) - _delta(ref[fin]))) <= 2e-5
+    rel = rel_err_arr(dpd[fin], ref[fin])
+    best = np.min([rel_err_arr(dpd[fin], o['disp_per_dist'][fin])
+                   for o in orders], axis=0)
+    ddelta = np.abs(_delta(dpd[fin]) - _delta(ref[fin]))
+    print('disp_per_dist: %d segments, %d > 1e-6 rel vs the reference (max '
+          '%.3g), %d > 1e-6 vs its nearest pixel order (max %.3g); max |d '
+          'delta| %.3g' % (rel.size, int(np.sum(rel > 1e-6)), rel.max(),
+                           int(np.sum(best > 1e-6)), best.max(),
+                           ddelta.max()))
+    assert np.sum(best > 1e-6) <= 1
+    assert ddelta.max() <= 1e-5
     s, t = g['sample_idx'], g['top_idx']
     # stage-isolated: the reference's table through the product's smoother,
     # LRT and BH
@@ -132,12 +158,18 @@ def test_cfg2_full_size_vs_reference(ctx, cfg2):
     for fdr in (0.01, 0.05, 0.1):
         np.testing.assert_array_equal(np.where(q < fdr)[0],
                                       g['calls_%g' % fdr])
-    # end to end
-    e2e_p, e2e_q = rel_err(out['pvalues'][s], g['p']), \
-        rel_err(out['qvalues'][s], g['q'])
-    print('end to end: sample p rel %.3g, q rel %.3g; top p rel %.3g' % (
-        e2e_p, e2e_q, rel_err(out['pvalues'][t], g['top_p'])))
-    assert e2e_p < 1e-3 and e2e_q < 1e-3
+    # end to end, against the reference's result under its nearest order
+    e2e = [max(rel_err(out['pvalues'][s], o['p_sample']),
+               rel_err(out['pvalues'][t], o['p_top']),
+               rel_err(out['qvalues'][s], o['q_sample']),
+               rel_err(out['qvalues'][t], o['q_top'])) for o in orders]
+    k = int(np.argmin(e2e))
+    print('end to end: vs the reference sample p rel %.3g, q rel %.3g, top p '
+          'rel %.3g; vs its nearest pixel order (%d) p / q rel %.3g' % (
+              rel_err(out['pvalues'][s], g['p']),
+              rel_err(out['qvalues'][s], g['q']),
+              rel_err(out['pvalues'][t], g['top_p']), k, e2e[k]))
+    assert e2e[k] < RTOL_PQ
     for fdr in (0.01, 0.05, 0.1):
         np.testing.assert_array_equal(np.where(out['qvalues'] < fdr)[0],
                                       g['calls_%g' % fdr])

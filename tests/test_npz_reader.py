@@ -148,3 +148,59 @@ def test_large_member_zip64(tmp_path):
                 np.lib.format.write_array(fh, np.asanyarray(arr))
     ref = _scipy_canonical(p)
     _same(_native.load_npz_csr(p), ref)
+
+
+def _write_npz(path, members):
+    import zipfile
+    with zipfile.ZipFile(path, 'w', compression=zipfile.ZIP_STORED) as z:
+        for name, arr in members:
+            with z.open(name + '.npy', 'w') as fh:
+                np.lib.format.write_array(fh, np.asanyarray(arr))
+
+
+def test_corrupt_indptr_is_rejected_before_any_row_is_read(tmp_path):
+    """indptr = [0, 10, 5] with nnz = 5: row 0 would scan indices[0..10)
+    past the buffer; the whole indptr is checked first (and a row after a
+    non-canonical one is still checked)."""
+    p = str(tmp_path / 'ip.npz')
+    _write_npz(p, [('indices', np.array([0, 1, 2, 3, 4], dtype=np.int32)),
+                   ('indptr', np.array([0, 10, 5], dtype=np.int64)),
+                   ('format', np.array('csr')), ('shape', np.array([2, 20])),
+                   ('data', np.ones(5))])
+    with pytest.raises(_native.H3DError, match='indptr'):
+        _native.load_npz_csr(p)
+    p2 = str(tmp_path / 'ip2.npz')   # row 0 unsorted, row 1 beyond nnz
+    _write_npz(p2, [('indices', np.array([3, 1, 2, 3, 4], dtype=np.int32)),
+                    ('indptr', np.array([0, 2, 9, 5], dtype=np.int64)),
+                    ('format', np.array('csr')),
+                    ('shape', np.array([3, 20])), ('data', np.ones(5))])
+    with pytest.raises(_native.H3DError, match='indptr'):
+        _native.load_npz_csr(p2)
+
+
+def test_directory_sizes_outside_the_file(tmp_path):
+    """File-supplied sizes are checked against the file before they size a
+    read or an allocation: a central-directory entry whose name length runs
+    past the directory, and a member claiming 4 GB uncompressed, are
+    H3DErrors (not an out-of-bounds read or an abort through bad_alloc)."""
+    m = sparse.random(50, 50, density=0.2, format='csr', random_state=1)
+    plain = str(tmp_path / 'plain.npz')
+    sparse.save_npz(plain, m, compressed=False)
+    raw = bytearray(open(plain, 'rb').read())
+    cd = raw.rfind(b'PK\x01\x02')              # last central-directory entry
+    bad = bytearray(raw)
+    bad[cd + 28:cd + 30] = (0xFFFF).to_bytes(2, 'little')   # name length
+    p = tmp_path / 'name.npz'
+    p.write_bytes(bytes(bad))
+    with pytest.raises(_native.H3DError):
+        _native.load_npz_csr(str(p))
+    big = bytearray(raw)
+    for k in range(4):                         # every member: usize 4 GB
+        off = big.find(b'PK\x01\x02', 0 if k == 0 else off + 4)
+        if off < 0:
+            break
+        big[off + 24:off + 28] = (0xFFFFFFF0).to_bytes(4, 'little')
+    p = tmp_path / 'usize.npz'
+    p.write_bytes(bytes(big))
+    with pytest.raises(_native.H3DError):
+        _native.load_npz_csr(str(p))
