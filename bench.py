@@ -403,11 +403,16 @@ def e2e_wall(h, tmp):
     t.append(time.perf_counter())
     h2.bh()
     t.append(time.perf_counter())
+    h2.flush()
+    t.append(time.perf_counter())
     return {'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
             'estimate_disp_s': t[2] - t[1], 'lrt_s': t[3] - t[2],
-            'bh_s': t[4] - t[3],
+            'bh_s': t[4] - t[3], 'outdir_flush_s': t[5] - t[4],
+            'estimate_disp_plus_lrt_s': t[3] - t[1],
             'note': 'HiC3DeFDR.run_to_qvalues stages on the bench workload, '
-                    'NPZ parse and .npy outdir writes included'}
+                    'NPZ parse included; the .npy outdir writes land on a '
+                    'background thread (write-behind) -- outdir_flush_s is '
+                    'the wait for the last of them, inside total_s'}
 
 
 def _outputs(torch, dev, n, C):
@@ -678,6 +683,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
                 'distance re-shard: all_to_all of the disp pixels, in-kernel '
                 'Brent per rank, table all-reduce' if by_dist
                 else 'per-pass NLL all-reduce over RCCL'), 'weak')
+        out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
         if world == 1:
             out['parity_vs_reference'] = parity_vs_reference(
                 ctx, o, n, args.bins, args.dmax, rank)
@@ -787,6 +793,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
                       'all-reduce), LRT on own chromosomes, genome-wide BH '
                       'as a sample sort over the ranks (two all_to_alls of '
                       'the p-values)'), 'strong')
+    out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
     out['config']['chromosomes_rank0'] = [int(i) for i in mine]
     out['config']['generate_s_rank0'] = gen_s
     if emu:

@@ -33,7 +33,7 @@ EXPORTS = [
     'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
     'h3d_estimate_disp_dev', 'h3d_bh_sort_dev', 'h3d_bh_scan_dev',
     'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
-    'h3d_disp_pixels_dev', 'h3d_table_gather_dev',
+    'h3d_disp_pixels_dev', 'h3d_table_gather_dev', 'h3d_disp_seg_stats',
 ]
 
 
@@ -96,6 +96,7 @@ def load_library(path=None):
             'h3d_disp_pixels_dev': (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _P,
                                          _I64, _I, _I64, _P, _P, _P]),
             'h3d_table_gather_dev': (_I, [_P, _P, _I, _I, _P, _I64, _P]),
+            'h3d_disp_seg_stats': (_I, [_P, _I, _P, _P]),
             'h3d_size_factors_cmor': (_I, [_P, _P, _P, _I64, _I, _I, _P]),
             'h3d_size_factors': (_I, [_P, _P, _P, _I64, _I, _I, _I, _P]),
             'h3d_disp_per_dist': (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _I,
@@ -303,6 +304,15 @@ class Context(object):
             n, R, n_disp, _P(d_raw_out) if d_raw_out else None,
             _P(d_f_out) if d_f_out else None,
             _P(d_dist_out) if d_dist_out else None), 'h3d_disp_pixels_dev')
+
+    def disp_seg_stats(self, D, C):
+        """(qcml iterations, Brent NLL evaluations) per segment (D, C) of
+        the last estimate_disp call on this ctx."""
+        qi = np.zeros((D, C), dtype=np.int32)
+        ev = np.zeros((D, C), dtype=np.int32)
+        _check(self.lib.h3d_disp_seg_stats(self.handle, D * C, _ptr(qi),
+                                           _ptr(ev)), 'h3d_disp_seg_stats')
+        return qi, ev
 
     def table_gather_dev(self, d_tables, D, C, d_dist, n, d_out):
         """disp = tables[dist] on the device (h3d_table_gather_dev)."""

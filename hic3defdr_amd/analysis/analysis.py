@@ -432,6 +432,8 @@ class AnalyzingHiC3DeFDR(object):
                            n_threads=n_threads)
         self.lrt(refit_mu=refit_mu, n_threads=n_threads, verbose=verbose)
         self.bh()
+        # every stage's outdir file has landed when the pipeline returns
+        self.flush()
 
     # ------------------------------------------------------------------
     def _chroms_for(self, chrom):

@@ -522,6 +522,14 @@ int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
                      int64_t* launches, int64_t* units) {
   if (!ctx || !name) return fail(H3D_EARG, "null argument");
   prof_collect(ctx);
+  if (std::strcmp(name, "gang_aborts") == 0) {
+    // gang Brent waits that hit their wall-clock bound (the searches then
+    // finished under k_brent): a count over the ctx's life, not a timing
+    if (total_ms) *total_ms = 0.0;
+    if (launches) *launches = ctx->gang_aborts;
+    if (units) *units = 0;
+    return 0;
+  }
   auto it = ctx->stats.find(name);
   ProfEntry e = (it == ctx->stats.end()) ? ProfEntry() : it->second;
   if (total_ms) *total_ms = e.ms;
@@ -1138,6 +1146,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   }
   std::memcpy(disp_per_dist, h_resd, (size_t)S * 8);
   std::memcpy(st.data(), h_sst, (size_t)S * sizeof(SegState));
+  ctx->last_S = S;
   const int bad = dev_tables ? *h_bad : 0;
   stamp("results");
   if (bad) return fail(H3D_EARG, "dist outside [0, %d)", D);
@@ -1242,6 +1251,18 @@ int h3d_disp_tables(const double* disp_per_dist, int D, int C, int weighted,
     if (rcs[c]) return fail(rcs[c], "condition %d: %s", c, errs[c].c_str());
   for (int c = 0; c < C; ++c)
     for (int d = 0; d < D; ++d) tables_out[(size_t)d * C + c] = outs[c][d];
+  return 0;
+}
+
+int h3d_disp_seg_stats(h3d_ctx* ctx, int S, int32_t* qiter, int32_t* evals) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  if (S != ctx->last_S || !ctx->h_res)
+    return fail(H3D_EARG, "no estimate_disp result of %d segments (last: %d)", S, ctx->last_S);
+  const SegState* h_sst = (const SegState*)((const double*)ctx->h_res + S);
+  for (int s = 0; s < S; ++s) {
+    if (qiter) qiter[s] = h_sst[s].qiter;
+    if (evals) evals[s] = h_sst[s].evals;
+  }
   return 0;
 }
 

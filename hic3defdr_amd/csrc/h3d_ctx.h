@@ -127,6 +127,9 @@ struct h3d_ctx {
   int gang_epoch = 0;
   void* gang_tag_buf = nullptr;
   size_t gang_tag_cap = 0;  // the tag allocation's capacity when last cleared
+  // segments of the last estimate_disp call whose final states are in h_res
+  // (h3d_disp_seg_stats)
+  int last_S = 0;
   h3dint::TablePending tab_pending;
   // H3D_DEV_SEG_TABLES (default 1): estimate_disp's chunk / segment tables
   // built on the device (k_disp_tables) where no gangs are needed

@@ -853,6 +853,24 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
 // partials read one by one cost ~20 us per evaluation (r03 A/B: 13.3 vs
 // 2.8 ms of Brent per cfg2 step).
 //
+// Ordering argument (why the relaxed pair is enough here). In the AMDGPU
+// memory model an agent-scope release is "buffer_wbl2 sc1; s_waitcnt
+// vmcnt(0)" and an acquire "s_waitcnt vmcnt(0); buffer_inv sc1": the L2
+// write-back / invalidate exist to make NON-atomic data visible across the
+// XCDs; the waitcnt orders the stores. Every datum this exchange publishes
+// is itself an agent-scope atomic (the partial and the tag), which the
+// hardware performs at the agent's coherence point rather than in a
+// non-coherent L2 line, so the only ordering left to enforce is that the
+// partial's store is complete before the tag's is issued -- the
+// s_waitcnt(0) between them (the signal fences keep the compiler from
+// moving either across it) -- and, on the reader's side, that the partial
+// loads are issued after the tag loads returned (the same waitcnt after the
+// poll). Those are the waitcnt halves of the release / acquire sequences.
+// The data the searches read otherwise (pseudodata, SegState) were written
+// by earlier kernels of the stream, ordered by the kernel boundary. A
+// bounded wait (below) still ends every gang if this ever failed to hold,
+// and the ctx counts such aborts (h3d_profile_read "gang_aborts").
+//
 // Progress: workgroups take tasks (segment, slice) from one queue in order,
 // the slices of a segment consecutive. A workgroup only waits for tasks of
 // its own segment; the segment at the queue head is the only one with both

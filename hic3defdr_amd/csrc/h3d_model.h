@@ -504,6 +504,8 @@ struct SegState {
   int flags;
   int num;
   int qiter;
+  int evals;  // NLL evaluations over every Brent search of the segment
+  int pad_;
   double disp;    // current qcml dispersion (used by the equalize pass)
   double x;       // delta at which the next NLL is evaluated
   double result;  // final qcml dispersion (NaN for an empty segment)
@@ -521,6 +523,8 @@ H3D_HD void seg_init(SegState* s, long long n_px, int n_reps) {
   s->flags = 0;
   s->num = 0;
   s->qiter = 0;
+  s->evals = 0;
+  s->pad_ = 0;
   s->disp = 0.01;
   s->x = brent_x0();
   s->k = nll_const(s->x, n_reps);
@@ -541,6 +545,7 @@ H3D_HD void seg_step(SegState* s, double total, int n_reps) {
   const double golden_mean = brent_golden();
   const double fval = -total;
   bool finished = false;
+  s->evals += 1;
   if (s->phase == kEqualize) {
     s->a = kBrentA;
     s->b = kBrentB;

@@ -67,18 +67,37 @@ class _CudaArray(object):
 
 def distance_owners(counts, world):
     """Rank owning each distance: LPT over the distances by their genome-wide
-    pixel counts (`counts`, (D,)), so every rank gets about the same number
-    of pixels (the equalize and NLL work of a distance is proportional to its
-    pixels). Deterministic: every rank computes the same table."""
-    counts = np.asarray(counts, dtype=np.int64)
+    weight (`counts`, (D,)): pixel counts, or the modelled / measured work of
+    each distance (``distance_cost``), so every rank gets about the same
+    work. Deterministic: every rank computes the same table from the same
+    weights."""
+    counts = np.asarray(counts)
+    counts = counts.astype(np.float64 if counts.dtype.kind == 'f'
+                           else np.int64)
     order = np.lexsort((np.arange(len(counts)), -counts))
-    loads = np.zeros(world, dtype=np.int64)
+    loads = np.zeros(world, dtype=counts.dtype)
     owner = np.zeros(len(counts), dtype=np.int32)
     for d in order:
         r = int(np.argmin(loads))        # first of the least loaded
         owner[d] = r
         loads[r] += counts[d]
     return owner
+
+
+def distance_cost(counts, count_sums, n_reps):
+    """A-priori work of each distance for ``distance_owners``: its pixels x
+    a per-pixel cost that grows with the distance's mean count per
+    pixel-replicate (``count_sums`` / (``counts`` x ``n_reps``)): the
+    q2qnbinom incomplete-gamma series / continued fractions run longer for
+    larger means (their trip counts grow like the square root of the gamma
+    shape mu / (1 + disp mu)), the Brent NLL passes do not. Calibrated on
+    the measured per-segment work of the cfg3 genome (tools/emulate_ranks.py,
+    profiles/r04/)."""
+    counts = np.asarray(counts, dtype=np.float64)
+    mu = np.asarray(count_sums, dtype=np.float64) / np.maximum(
+        counts * n_reps, 1.0)
+    shape = mu / (1.0 + 0.05 * mu)
+    return counts * (1.0 + 0.35 * np.sqrt(shape))
 
 
 def _xdev(dev, group=None):
@@ -213,7 +232,11 @@ class Shards(object):
 
     @property
     def sharded(self):
-        return self.world > 1
+        # H3D_FORCE_SHARDED=1: the sharded paths (distance re-shard, sharded
+        # BH) even at world size 1 -- a test hook, so that the collectives run
+        # under RCCL on a one-GPU box (tests/test_gpu_multirank.py)
+        return self.world > 1 or (self.dist is not None and
+                                  os.environ.get('H3D_FORCE_SHARDED') == '1')
 
     def barrier(self):
         if self.dist is not None:

@@ -183,6 +183,12 @@ int h3d_disp_per_dist_dev(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                           double* disp_per_dist, int32_t* seg_flags,
                           h3d_allreduce_fn reduce, void* user);
 
+/* Work of the last h3d_disp_per_dist[_dev] / h3d_estimate_disp_dev call on
+ * the ctx, per (distance, condition) segment s = d * C + c (S = D * C):
+ * qcml iterations (equalize passes) and bounded-Brent NLL evaluations. The
+ * multi-GPU distance owners balance on these (measurement). */
+int h3d_disp_seg_stats(h3d_ctx* ctx, int S, int32_t* qiter, int32_t* evals);
+
 /* Smoothed dispersion function of one condition, tabulated at d = 0..D-1
  * (lowess.py:95-244 weighted_lowess_fit if weighted, else lowess_fit;
  * left_boundary = first finite value, as analysis.py:212). frac < 0 = auto. */
@@ -358,7 +364,8 @@ int h3d_mme_per_pixel(h3d_ctx* ctx, const double* data, const double* f,
  * equalize pass), "disp_nll", "disp_reduce", "disp_update", "disp_prep",
  * "lrt"}. units: algorithmic HBM bytes for "disp_work" / "disp_nll"
  * (counted on the device since the last reset), pixels for "lrt" /
- * "disp_prep". */
+ * "disp_prep". name "gang_aborts": *launches = gang Brent waits of the ctx
+ * that timed out (the searches then finished under k_brent). */
 int h3d_profile_enable(h3d_ctx* ctx, int on);
 int h3d_profile_read(h3d_ctx* ctx, const char* name, double* total_ms,
                      int64_t* launches, int64_t* units);

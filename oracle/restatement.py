@@ -656,6 +656,48 @@ def poisson_lrt(raw, f, design):
 
 
 # --------------------------------------------------------------------------
+# evaluation — reference util/evaluation.py
+# --------------------------------------------------------------------------
+
+
+def make_y_true(row, col, clusters, labels):
+    """``evaluation.py:15-41``: the reference's set union and per-pixel
+    membership loop."""
+    labels = np.asarray(labels)
+    sig_idx = ~(labels == 'constit')
+    sig_pixels = set().union(*[set(map(tuple, c)) for i, c in
+                               enumerate(clusters) if sig_idx[i]])
+    return np.array([(r, c) in sig_pixels for r, c in zip(row, col)],
+                    dtype=bool)
+
+
+def compute_fdr(y_true, y_pred):
+    """``evaluation.py:82-100``: fp / (fp + tp) of the confusion matrix."""
+    from sklearn.metrics import confusion_matrix
+    tn, fp, fn, tp = confusion_matrix(y_true, y_pred,
+                                      labels=[False, True]).ravel()
+    return fp / float(fp + tp)
+
+
+def evaluate(y_true, qvalues, n_fdr_points=100):
+    """``evaluation.py:44-79``: sklearn's ROC on 1 - q and the FDR by a
+    confusion matrix at every ``rate``-th threshold from the first with tpr
+    > 0. The first threshold is the reference's scikit-learn 0.24 value (the
+    largest score + 1; scikit-learn >= 1.3 opens at +inf)."""
+    from sklearn.metrics import roc_curve
+    y_pred = 1 - qvalues
+    fpr, tpr, thresh = roc_curve(y_true, y_pred)
+    if len(thresh) and np.isinf(thresh[0]):
+        thresh = thresh.copy()
+        thresh[0] = thresh[1] + 1 if len(thresh) > 1 else 1.0
+    fdr = np.ones_like(fpr) * np.nan
+    rate = max(int(len(thresh) / n_fdr_points), 1)
+    for i in range(np.argmax(tpr > 0), len(thresh), rate):
+        fdr[i] = compute_fdr(y_true, y_pred >= thresh[i])
+    return fdr, fpr, tpr, thresh
+
+
+# --------------------------------------------------------------------------
 # pipeline driver — reference analysis/analysis.py + analysis/core.py
 # --------------------------------------------------------------------------
 

@@ -1,9 +1,10 @@
-"""torchrun worker for tests/test_gpu_dist.py: the product's sharded
+"""torchrun worker for tests/test_gpu_multirank.py: the product's sharded
 HiC3DeFDR.run_to_qvalues() on a golden dataset, one rank per process, every
 rank on the GPU H3D_DEVICE names, backend gloo (several ranks on one GPU;
-RCCL refuses duplicate devices).
+RCCL refuses duplicate devices) or nccl (= RCCL; one rank per GPU, so on a
+one-GPU box world 1 with H3D_FORCE_SHARDED=1).
 
-    torchrun --nproc-per-node 2 tests/dist_product_main.py <name> <outdir>
+    torchrun --nproc-per-node 2 tests/dist_product_main.py <name> <outdir> [gloo|nccl]
 """
 import os
 import sys
@@ -18,8 +19,15 @@ def main():
     import torch.distributed as dist
     from conftest import e2e_inputs
     from hic3defdr_amd import HiC3DeFDR
+    import torch
     name, outdir = sys.argv[1], sys.argv[2]
-    dist.init_process_group('gloo')
+    backend = sys.argv[3] if len(sys.argv) > 3 else 'gloo'
+    if backend == 'nccl':
+        dev = torch.device('cuda', int(os.environ.get('H3D_DEVICE', '0')))
+        torch.cuda.set_device(dev)
+        dist.init_process_group('nccl', device_id=dev)
+    else:
+        dist.init_process_group('gloo')
     _, kw = e2e_inputs(name)
     design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
     h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
@@ -28,7 +36,9 @@ def main():
                   dist_thresh_max=kw['dist_thresh_max'],
                   loop_patterns=kw['loop_patterns'], res=10000)
     sh = h._shards()
-    print('rank %d of %d owns %s' % (sh.rank, sh.world, sh.mine), flush=True)
+    print('rank %d of %d owns %s (backend %s, sharded paths %s)' % (
+        sh.rank, sh.world, sh.mine, dist.get_backend(), sh.sharded),
+        flush=True)
     h.run_to_qvalues(verbose=False)
     dist.barrier()
     dist.destroy_process_group()

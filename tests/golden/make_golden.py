@@ -667,6 +667,89 @@ def run_full_cfg2(bins=20000, dmax=250, seed=0, chunk=20000, n_sample=50000):
           {k: len(v) for k, v in out.items() if k.startswith('calls_')})
 
 
+CFG1 = {'chr18': 9070, 'chr19': 6143}   # mm10 chr18 / chr19 at 10 kb
+
+
+def run_full_cfg1(dmax=200, seed=7, chunk=20000, n_sample=20000,
+                  fdrs=(0.01, 0.05), sizes=(3, 4)):
+    """BASELINE configs[0]'s shape at full size (the Bonev demo's chr18 +
+    chr19 at 10 kb, R = 4 as 2 + 2, dist_thresh_max 200; synthetic data of
+    that shape, with loop clusters, since the demo data is not available
+    offline) through the REFERENCE: prepare_data and estimate_disp over both
+    chromosomes (analysis.py:28-223), its util/lrt.py:7-50 lrt per
+    chromosome in chunks of `chunk` pixels (as run_full_cfg2; the outputs
+    saved where its lrt() saves them, analysis.py:281-284), bh() over the
+    loop pixels of both chromosomes (:286-303) and collect() (:498-572:
+    threshold, classify, the results TSV) at every (fdr, cluster size).
+    full_cfg1.npz: disp_per_dist, per chromosome a seeded sample of disp
+    pixels with p / llr / mu0 / mu1, every loop pixel's q, the call sets,
+    and the text of every results_<fdr>_<size>.tsv."""
+    import multiprocessing
+    # (the inputs are regenerated from the seed by the test, as full_cfg2's)
+    base = os.path.join('/tmp', 'h3golden_cfg1_data')
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, CFG1, dist_thresh_max=dmax, seed=seed)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_cfg1_out')
+    shutil.rmtree(outdir, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax,
+                  loop_patterns=kw['loop_patterns'], res=10000)
+    h.prepare_data(n_threads=-1, verbose=False)
+    h.estimate_disp(n_threads=-1)
+    dsg = design.values
+    rng = np.random.default_rng(seed)
+    out = {'meta_chroms': np.array(kw['chroms']),
+           'meta_bins': np.array([CFG1[c] for c in kw['chroms']]),
+           'meta_dmax': np.array(dmax), 'meta_seed': np.array(seed),
+           'meta_lrt_chunk': np.array(chunk), 'meta_equal_bin': np.array('stable'),
+           'disp_per_dist': np.load(os.path.join(outdir, 'disp_per_dist.npy'))}
+    for chrom in kw['chroms']:
+        bias = h.load_bias(chrom)
+        sf = h.load_data('size_factors', chrom)
+        di = h.load_data('disp_idx', chrom)
+        row = h.load_data('row', chrom, idx=di)
+        col = h.load_data('col', chrom, idx=di)
+        raw = h.load_data('raw', chrom, idx=di)
+        disp = h.load_data('disp', chrom)
+        f = bias[row] * bias[col] * sf[di, :]
+        dw = np.dot(disp, dsg.T)
+        n = len(raw)
+        bounds = list(range(0, n, chunk)) + [n]
+        tasks = [(raw[a:b], f[a:b], dw[a:b], dsg)
+                 for a, b in zip(bounds[:-1], bounds[1:])]
+        with multiprocessing.get_context('fork').Pool(8) as pool:
+            res = pool.map(_ref_lrt_chunk, tasks, chunksize=1)
+        p, llr, m0, m1 = (np.concatenate([r[i] for r in res])
+                          for i in range(4))
+        for name, a in (('pvalues', p), ('llr', llr), ('mu_hat_null', m0),
+                        ('mu_hat_alt', m1)):
+            h.save_data(a, name, chrom)
+        s = np.sort(rng.choice(n, size=min(n_sample, n), replace=False))
+        out.update({'n_disp__%s' % chrom: np.array(n),
+                    'sample_idx__%s' % chrom: s.astype(np.int32),
+                    'p__%s' % chrom: p[s], 'llr__%s' % chrom: llr[s],
+                    'mu0__%s' % chrom: m0[s], 'mu1__%s' % chrom: m1[s]})
+    h.bh()
+    for chrom in kw['chroms']:
+        q = h.load_data('qvalues', chrom)
+        out['q__%s' % chrom] = q
+        out['loop_idx__%s' % chrom] = h.load_data('loop_idx', chrom)
+    h.collect(fdr=list(fdrs), cluster_size=list(sizes))
+    for fdr in fdrs:
+        for size in sizes:
+            with open(os.path.join(outdir, 'results_%g_%i.tsv' % (fdr, size))) \
+                    as fh:
+                out['results_%g_%i' % (fdr, size)] = np.array(fh.read())
+    np.savez_compressed(os.path.join(HERE, 'full_cfg1.npz'), **out)
+    print('full cfg1:', {c: int(out['n_disp__%s' % c]) for c in kw['chroms']},
+          'loop pixels', {c: int(out['loop_idx__%s' % c].sum())
+                          for c in kw['chroms']},
+          'results lines', {k: str(v).count('\n') for k, v in out.items()
+                            if k.startswith('results_')})
+
+
 class _PermutedQcml(object):
     """qcml (dispersion.py:10-43) on the segment's pixels in a seeded
     permutation of their order. The result should not depend on the order
@@ -759,6 +842,69 @@ def run_cfg2_spread(bins=20000, dmax=250, seed=0, perms=(0, 1, 2, 3, 4, 5),
               flush=True)
     dispersion.qcml = dispersion.__dict__['_orig_qcml']
     np.savez_compressed(os.path.join(HERE, 'cfg2_spread.npz'), **out)
+
+
+SIM_SCALE = {'chr1': 19535, 'chr2': 18211, 'chr3': 16007}  # mm10, 10 kb
+
+
+def csr_digest(m):
+    """sha256 of a CSR matrix's canonical arrays (indptr int64, indices
+    int32, data int64) -- the same function in tests/test_gpu_sim_scale.py."""
+    import hashlib
+    h = hashlib.sha256()
+    for a, dt in ((m.indptr, np.int64), (m.indices, np.int32),
+                  (m.data, np.int64)):
+        h.update(np.ascontiguousarray(a, dtype=dt).tobytes())
+    return h.hexdigest()
+
+
+def run_sim_scale(dmax=200, seed=11, sim_seed=42):
+    """BASELINE configs[4] (simulate-based truth set) at the genome's scale:
+    three full-size mm10 chromosomes (chr1-3 at 10 kb, R = 4 as 2 + 2, dmax
+    200, loop clusters). The REFERENCE's prepare_data + estimate_disp on
+    them, then its simulate('ES') (analysis/simulation.py:22-144 ->
+    util/simulation.py:70-204) with np.random.seed(sim_seed), serially (the
+    stream is consumed chromosome by chromosome). sim_scale.npz: the
+    reference's disp_per_dist, the cluster labels, and per simulated
+    replicate and chromosome the sha256 of its CSR arrays, nnz, the count
+    sum and the first 2,000 stored counts (the matrices themselves are ~40 M
+    entries)."""
+    import scipy.sparse as sp
+    base = os.path.join('/tmp', 'h3golden_simscale_data')
+    shutil.rmtree(base, ignore_errors=True)
+    kw = synthetic.write_dataset(base, SIM_SCALE, dist_thresh_max=dmax,
+                                 seed=seed)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    outdir = os.path.join('/tmp', 'h3golden_simscale_out')
+    simdir = os.path.join('/tmp', 'h3golden_simscale_sim')
+    for d in (outdir, simdir):
+        shutil.rmtree(d, ignore_errors=True)
+    h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                  bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                  design=design, outdir=outdir, dist_thresh_max=dmax,
+                  loop_patterns=kw['loop_patterns'])
+    h.prepare_data(n_threads=-1, verbose=False)
+    h.estimate_disp(n_threads=-1)
+    np.random.seed(sim_seed)
+    h.simulate('ES', outdir=simdir, n_threads=0, verbose=False)
+    out = {'meta_seed': np.array(seed), 'meta_sim_seed': np.array(sim_seed),
+           'meta_dmax': np.array(dmax), 'meta_cond': np.array('ES'),
+           'meta_chroms': np.array(kw['chroms']),
+           'disp_per_dist': np.load(os.path.join(outdir, 'disp_per_dist.npy'))}
+    for chrom in kw['chroms']:
+        out['labels__%s' % chrom] = np.loadtxt(
+            os.path.join(simdir, 'labels_%s.txt' % chrom), dtype='U7')
+        for rep in ('A1', 'A2', 'B1', 'B2'):
+            m = sp.load_npz(os.path.join(simdir, '%s_%s_raw.npz'
+                                         % (rep, chrom))).tocsr()
+            key = '%s__%s' % (rep, chrom)
+            out['sha256__' + key] = np.array(csr_digest(m))
+            out['nnz__' + key] = np.array(m.nnz)
+            out['sum__' + key] = np.array(int(m.data.sum()))
+            out['head__' + key] = np.asarray(m.data[:2000], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, 'sim_scale.npz'), **out)
+    print('sim scale:', {k: int(v) for k, v in out.items()
+                         if k.startswith('nnz__')})
 
 
 SIM_EVALS = [(None, None, False), (None, 15, False), (16, 30, True),
@@ -868,6 +1014,10 @@ if __name__ == '__main__':
         run_full_cfg2()
     if 'cfg2_spread' in which:
         run_cfg2_spread()
+    if 'full_cfg1' in which:
+        run_full_cfg1()
+    if 'sim_scale' in which:
+        run_sim_scale()
     if 'sim' in which:
         run_sim()
     if 'alt' in which:

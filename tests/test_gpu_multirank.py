@@ -5,9 +5,15 @@ it; estimate_disp runs either the distance re-shard (default: one
 all_to_all of the disp pixels, the single-GPU driver per rank, one table
 all-reduce; parallel.disp_per_dist_by_distance) or the device driver's
 multi-rank branch (H3D_DISP_SHARD=pass: per-pass all-reduce of the NLL sums
-through parallel.make_allreduce on torch's stream); BH gathers on rank 0 and
-scatters back. The outdir must match the
-reference goldens like the single-rank run does (tests/test_gpu_e2e.py).
+through parallel.make_allreduce on torch's stream); BH is the sample sort
+over the ranks (parallel.bh_sharded: all_gathers of splitters and bucket
+counts, two all_to_alls). The outdir must match the reference goldens like
+the single-rank run does (tests/test_gpu_e2e.py). The same product run
+under RCCL ('nccl'): one rank (RCCL takes one GPU per rank) with the
+sharded paths forced, so the distance re-shard's uneven all_to_all_single,
+the table all-reduce and bh_sharded's all_gathers / all_to_alls execute on
+RCCL and the stream hand-off between libh3d and the collectives is
+exercised.
 
 The ranks start from the pytest process after the other GPU tests have run
 in it (the file sorts among them; the parent holds a torch CUDA context and
@@ -36,24 +42,31 @@ from conftest import REPO, e2e_inputs, rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('shard', ['distance', 'pass'])
+@pytest.mark.parametrize('shard,backend', [('distance', 'gloo'),
+                                           ('pass', 'gloo'),
+                                           ('distance', 'nccl')])
 @pytest.mark.parametrize('name', ['small2'])
-def test_two_ranks_run_to_qvalues_matches_reference(name, shard):
+def test_two_ranks_run_to_qvalues_matches_reference(name, shard, backend):
     g, kw = e2e_inputs(name)
     assert len(kw['chroms']) == 2   # one chromosome per rank
+    ranks = 2 if backend == 'gloo' else 1
     outdir = tempfile.mkdtemp(prefix='h3d_dist_')
     try:
         env = dict(os.environ, H3D_DEVICE='0', MASTER_ADDR='127.0.0.1',
                    OMP_NUM_THREADS='1', H3D_DEBUG='1')
         env.pop('H3D_DISP_SHARD', None)
+        env.pop('H3D_FORCE_SHARDED', None)
         if shard == 'pass':
             env['H3D_DISP_SHARD'] = 'pass'
-        port = 29600 + os.getpid() % 1000 + (7 if shard == 'pass' else 0)
+        if backend == 'nccl':
+            env['H3D_FORCE_SHARDED'] = '1'
+        port = 29600 + os.getpid() % 1000 + (7 if shard == 'pass' else 0) + \
+            (13 if backend == 'nccl' else 0)
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
-               '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+               '--nproc-per-node', str(ranks), '--master-addr', '127.0.0.1',
                '--master-port', str(port),
                os.path.join(REPO, 'tests', 'dist_product_main.py'), name,
-               outdir]
+               outdir, backend]
         log = os.path.join(outdir, 'ranks.log')
         with open(log, 'w') as fh:
             try:
@@ -65,9 +78,13 @@ def test_two_ranks_run_to_qvalues_matches_reference(name, shard):
         text = open(log).read()
         assert rc == 0, text[-4000:]
         # the two ranks share one log: their lines may interleave
-        owned = sorted(re.findall(r"rank \d of 2 owns \[[^\]]*\]", text))
-        assert len(owned) == 2 and "['chrA']" in ' '.join(owned) and \
-            "['chrB']" in ' '.join(owned), owned
+        owned = sorted(re.findall(r"rank \d of %d owns \[[^\]]*\]" % ranks,
+                                  text))
+        assert len(owned) == ranks and "'chrA'" in ' '.join(owned) and \
+            "'chrB'" in ' '.join(owned), owned
+        assert 'sharded paths True' in text, text[-2000:]
+        if backend == 'nccl':
+            assert 'backend nccl' in text, text[-2000:]
         dpd = np.load(os.path.join(outdir, 'disp_per_dist.npy'))
         np.testing.assert_allclose(dpd, g['disp_per_dist'], rtol=1e-6,
                                    atol=1e-12)

@@ -1,0 +1,150 @@
+"""BASELINE configs[4] -- the simulate()-based truth set -- at the genome's
+scale: three full-size mm10 chromosomes (chr1-3 at 10 kb, 53,753 bins, R =
+4 as 2 + 2, dist_thresh_max 200, loop clusters), regenerated from their
+seed.
+
+1. The product's prepare_data (GPU) and the REFERENCE's dispersion
+   function (tests/golden/sim_scale.npz: its disp_per_dist, smoothed by the
+   product's smoother, bit-equal to the reference's on that input) feed the
+   product's simulate('ES') (analysis/simulation.py:22-144,
+   util/simulation.py:70-204) with the reference's seed: every simulated
+   replicate of every chromosome is the reference's, count for count (sha256
+   of the CSR arrays), and the cluster labels are identical. The reference's
+   own disp_fn isolates the sampler from estimate_disp, whose segments may
+   land elsewhere inside Brent's tolerance (test_gpu_scale.py).
+2. The GPU analysis of the simulated set (run_to_qvalues, the simulated
+   replicates biased by their source replicates' bias vectors), timed, and
+   evaluate() on its q-values against the oracle's evaluate (the reference's
+   loops, pinned to its eval.npz by test_simulation.py) on the same
+   q-values: fdr / fpr / tpr / thresh identical."""
+import hashlib
+import os
+import shutil
+import tempfile
+import time
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+SIM_SCALE = {'chr1': 19535, 'chr2': 18211, 'chr3': 16007}
+SIMREPS = ['A1', 'A2', 'B1', 'B2']
+
+
+def csr_digest(m):
+    """sha256 of a CSR matrix's canonical arrays (make_golden.csr_digest)."""
+    h = hashlib.sha256()
+    for a, dt in ((m.indptr, np.int64), (m.indices, np.int32),
+                  (m.data, np.int64)):
+        h.update(np.ascontiguousarray(a, dtype=dt).tobytes())
+    return h.hexdigest()
+
+
+@pytest.fixture(scope='module')
+def simulated():
+    from hic3defdr_amd import HiC3DeFDR, _native, synthetic
+    from hic3defdr_amd.analysis.core import DispFn
+    g = golden('sim_scale.npz')
+    tmp = tempfile.mkdtemp(prefix='h3d_simscale_')
+    try:
+        dmax = int(g['meta_dmax'])
+        kw = synthetic.write_dataset(tmp, SIM_SCALE, dist_thresh_max=dmax,
+                                     seed=int(g['meta_seed']))
+        design = pd.DataFrame(kw['design'], index=kw['reps'],
+                              columns=kw['conds'])
+        h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                      bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                      design=design, outdir=os.path.join(tmp, 'out'),
+                      dist_thresh_max=dmax, loop_patterns=kw['loop_patterns'])
+        t0 = time.perf_counter()
+        h.prepare_data(verbose=False)
+        t_prep = time.perf_counter() - t0
+        dpd = g['disp_per_dist']
+        tables = _native.disp_tables(dpd)
+        for c, cond in enumerate(design.columns):
+            h.save_disp_fn(cond, DispFn(tables[:, c], dpd[:, c]))
+        sim = os.path.join(tmp, 'sim')
+        np.random.seed(int(g['meta_sim_seed']))
+        t0 = time.perf_counter()
+        h.simulate('ES', outdir=sim, verbose=False)
+        t_sim = time.perf_counter() - t0
+        print('prepare_data %.2f s, simulate %.2f s' % (t_prep, t_sim))
+        yield h, g, kw, sim, tmp
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_simulated_counts_are_the_references(simulated):
+    import scipy.sparse as sparse
+    h, g, kw, sim, _ = simulated
+    for chrom in kw['chroms']:
+        np.testing.assert_array_equal(
+            np.loadtxt(os.path.join(sim, 'labels_%s.txt' % chrom), dtype='U7'),
+            g['labels__%s' % chrom])
+        for rep in SIMREPS:
+            m = sparse.load_npz(os.path.join(sim, '%s_%s_raw.npz'
+                                             % (rep, chrom))).tocsr()
+            key = '%s__%s' % (rep, chrom)
+            assert m.nnz == int(g['nnz__' + key]), key
+            assert int(m.data.sum()) == int(g['sum__' + key]), key
+            np.testing.assert_array_equal(m.data[:2000], g['head__' + key])
+            assert csr_digest(m) == str(g['sha256__' + key]), key
+
+
+def test_analysis_of_the_simulated_set_and_evaluate(simulated):
+    import oracle
+    from hic3defdr_amd import HiC3DeFDR
+    h, g, kw, sim, tmp = simulated
+    # the simulated replicates carry the source replicates' biases
+    # (simulate's np.tile(bias, 2): A1 / B1 <- ES1, A2 / B2 <- ES2)
+    src = [p for p, on in zip(kw['bias_patterns'], h.design['ES']) if on]
+    bias_patterns = src + src
+    hs = HiC3DeFDR(
+        raw_npz_patterns=[os.path.join(sim, '%s_<chrom>_raw.npz' % r)
+                          for r in SIMREPS],
+        bias_patterns=bias_patterns, chroms=kw['chroms'],
+        design=os.path.join(sim, 'design.csv'),
+        outdir=os.path.join(tmp, 'simout'),
+        dist_thresh_max=int(g['meta_dmax']),
+        loop_patterns={'ES': kw['loop_patterns']['ES']})
+    t = [time.perf_counter()]
+    hs.prepare_data(verbose=False)
+    t.append(time.perf_counter())
+    hs.estimate_disp()
+    t.append(time.perf_counter())
+    hs.lrt(verbose=False)
+    t.append(time.perf_counter())
+    hs.bh()
+    t.append(time.perf_counter())
+    hs.flush()
+    t.append(time.perf_counter())
+    n_disp = sum(int(hs.load_data('disp_idx', c).sum()) for c in kw['chroms'])
+    print('simulated set: %d disp pixels; prepare_data %.2f s, estimate_disp '
+          '%.2f s, lrt %.2f s, bh %.2f s, outdir flush %.2f s' % (
+              (n_disp,) + tuple(b - a for a, b in zip(t[:-1], t[1:]))))
+    hs.evaluate('ES', os.path.join(sim, 'labels_<chrom>.txt'))
+    e = np.load(os.path.join(tmp, 'simout', 'eval.npz'))
+    ys, qs = [], []
+    for c in kw['chroms']:
+        di = hs.load_data('disp_idx', c)
+        li = hs.load_data('loop_idx', c)
+        sel = np.flatnonzero(di)[li]
+        row = hs.load_data('row', c)[sel]
+        col = hs.load_data('col', c)[sel]
+        cl = oracle.load_clusters(kw['loop_patterns']['ES'].replace('<chrom>', c))
+        ys.append(oracle.make_y_true(row, col, cl, np.loadtxt(
+            os.path.join(sim, 'labels_%s.txt' % c), dtype='U7')))
+        qs.append(hs.load_data('qvalues', c))
+    y, q = np.concatenate(ys), np.concatenate(qs)
+    assert y.sum() > 100 and np.all(np.isfinite(q))
+    ref = oracle.evaluate(y, q)
+    for k, v in zip(('fdr', 'fpr', 'tpr', 'thresh'), ref):
+        np.testing.assert_array_equal(np.isnan(e[k]), np.isnan(v))
+        np.testing.assert_allclose(e[k], v, rtol=1e-12, atol=0)
+    print('evaluate: %d loop pixels (%d true), %d ROC points; tpr at fpr <= '
+          '0.05: %.3f' % (len(y), int(y.sum()), len(e['fpr']),
+                          float(e['tpr'][e['fpr'] <= 0.05].max())))

@@ -135,3 +135,28 @@ def test_evaluate_matches_reference(which):
             np.testing.assert_allclose(e[k], ref, rtol=1e-12, atol=0)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_oracle_evaluate_matches_reference():
+    """The oracle's evaluate / make_y_true (the reference's own loops,
+    oracle/restatement.py) pinned to the reference's eval.npz on its own
+    simulated-analysis q-values: the checker test_gpu_sim_scale.py uses at
+    the genome's scale."""
+    import oracle
+    g = golden('sim_small2.npz')
+    _, kw = e2e_inputs('small2')
+    ys, qs = [], []
+    for c in kw['chroms']:
+        di = g['simrun__disp_idx__%s' % c]
+        li = g['simrun__loop_idx__%s' % c]
+        sel = np.flatnonzero(di)[li]
+        row = g['simrun__row__%s' % c][sel]
+        col = g['simrun__col__%s' % c][sel]
+        cl = oracle.load_clusters(kw['loop_patterns']['ES'].replace('<chrom>', c))
+        ys.append(oracle.make_y_true(row, col, cl, g['labels__%s' % c]))
+        qs.append(g['simrun__qvalues__%s' % c])
+    e = oracle.evaluate(np.concatenate(ys), np.concatenate(qs))
+    for k, v in zip(('fdr', 'fpr', 'tpr', 'thresh'), e):
+        ref = g['eval__eval__%s' % k]
+        np.testing.assert_array_equal(np.isnan(v), np.isnan(ref))
+        np.testing.assert_allclose(v, ref, rtol=1e-12, atol=0)
