@@ -707,6 +707,59 @@ static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int 
   seg_step(s, total, n_reps);
 }
 
+// One thread's share of a segment's NLL terms at one Brent trial point:
+// pixels [b, el) from the LDS head, [el, e) from memory, two pixels per
+// iteration (px, px + block): their lgammas are independent chains the
+// scheduler interleaves (the NLL is bound by FP64 dependency latency at 4
+// waves/SIMD); the terms still join the sum in pixel order (M >= 8: one
+// pixel per trip -- the pair spilled at the 128-VGPR budget of
+// __launch_bounds__(512, 4)). LARGE: every argument >= kNllLargeR
+// (nll_pixel_large).
+template <int M, int kBlockT, bool LARGE>
+__device__ __forceinline__ double brent_segment_sum(
+    const double* s_pd, int64_t lds_px, const double* __restrict__ pd, int64_t n,
+    const int* ri, int nr, int64_t b, int64_t el, int64_t e, const NllConst& kc,
+    const LogTab* s_tab) {
+  double acc = 0.0;
+  constexpr int kPair = M <= 4 ? 2 : 1;
+  auto term = [&](const double* v) {
+    return LARGE ? nll_pixel_large<M>(v, nr, kc, s_tab) : nll_pixel<M>(v, nr, kc, s_tab);
+  };
+  for (int64_t i = threadIdx.x; i < el - b; i += kPair * kBlockT) {
+    const int64_t j = i + kBlockT;
+    const bool two = kPair == 2 && j < el - b;
+    double v[M], w[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      v[k] = (k < nr) ? s_pd[k * lds_px + i] : 0.0;
+      w[k] = (k < nr && two) ? s_pd[k * lds_px + j] : 0.0;
+    }
+    const double t0 = term(v);
+    acc += t0;
+    if constexpr (kPair == 2) {
+      const double t1 = term(w);
+      if (two) acc += t1;
+    }
+  }
+  for (int64_t px = el + threadIdx.x; px < e; px += kPair * kBlockT) {
+    const int64_t qx = px + kBlockT;
+    const bool two = kPair == 2 && qx < e;
+    double v[M], w[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
+      w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
+    }
+    const double t0 = term(v);
+    acc += t0;
+    if constexpr (kPair == 2) {
+      const double t1 = term(w);
+      if (two) acc += t1;
+    }
+  }
+  return acc;
+}
+
 // The segment's first `lds_px` pixels are staged in LDS once per search (the
 // dynamic shared buffer, up to ~150 KB: one 1024-thread workgroup per CU);
 // every evaluation reads them from there and streams only the rest -- the
@@ -767,49 +820,15 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     __syncthreads();
     while (true) {
       const NllConst kc = s_st.k;
-      double acc = 0.0;
-      // two pixels per iteration (px, px + block): their lgammas are
-      // independent chains the scheduler interleaves (the NLL is bound by
-      // FP64 dependency latency at 4 waves/SIMD); the terms still join the
-      // sum in pixel order
-      // (M >= 8: one pixel per trip -- the pair spilled at the 128-VGPR
-      // budget of __launch_bounds__(512, 4))
-      constexpr int kPair = M <= 4 ? 2 : 1;
-      for (int64_t i = threadIdx.x; i < el - b; i += kPair * kBrentBlock) {
-        const int64_t j = i + kBrentBlock;
-        const bool two = kPair == 2 && j < el - b;
-        double v[M], w[M];
+      // every lgamma argument >= r: at r >= kNllLargeR the short path
+      // (nll_pixel_large), the same for every thread of the segment
+      const double acc = (kc.r >= kNllLargeR)
+          ? brent_segment_sum<M, kBrentBlock, true>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
+          : brent_segment_sum<M, kBrentBlock, false>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab);
+      double wacc = acc;
 #pragma unroll
-        for (int k = 0; k < M; ++k) {
-          v[k] = (k < nr) ? s_pd[k * lds_px + i] : 0.0;
-          w[k] = (k < nr && two) ? s_pd[k * lds_px + j] : 0.0;
-        }
-        const double t0 = nll_pixel<M>(v, nr, kc, s_tab);
-        acc += t0;
-        if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
-          if (two) acc += t1;
-        }
-      }
-      for (int64_t px = el + threadIdx.x; px < e; px += kPair * kBrentBlock) {
-        const int64_t qx = px + kBrentBlock;
-        const bool two = kPair == 2 && qx < e;
-        double v[M], w[M];
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
-          w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
-        }
-        const double t0 = nll_pixel<M>(v, nr, kc, s_tab);
-        acc += t0;
-        if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
-          if (two) acc += t1;
-        }
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) wpart[wid] = acc;
+      for (int off = 32; off > 0; off >>= 1) wacc += __shfl_xor(wacc, off, 64);
+      if (lane == 0) wpart[wid] = wacc;
       __syncthreads();
       if (threadIdx.x == 0) {
         double total = 0.0;
@@ -935,25 +954,10 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
     __syncthreads();
     while (true) {
       const NllConst kc = s_st.k;
-      double acc = 0.0;
-      // the slice, two pixels per trip for M <= 4 (independent lgamma
-      // chains), as k_brent
-      constexpr int kPair = M <= 4 ? 2 : 1;
-      for (int64_t px = sb + threadIdx.x; px < se; px += kPair * kGangThreads) {
-        const int64_t qx = px + kGangThreads;
-        const bool two = kPair == 2 && qx < se;
-        double v[M], w[M];
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-          v[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
-          w[k] = (k < nr && two) ? pd[(int64_t)ri[k] * n + qx] : 0.0;
-        }
-        acc += nll_pixel<M>(v, nr, kc, s_tab);
-        if constexpr (kPair == 2) {
-          const double t1 = nll_pixel<M>(w, nr, kc, s_tab);
-          if (two) acc += t1;
-        }
-      }
+      // the slice (no LDS head), two pixels per trip for M <= 4, as k_brent
+      double acc = (kc.r >= kNllLargeR)
+          ? brent_segment_sum<M, kGangThreads, true>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab)
+          : brent_segment_sum<M, kGangThreads, false>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) wpart[wid] = acc;

@@ -459,6 +459,25 @@ H3D_HD NllConst nll_const(double delta, int n) {
 // far inside the double range (P < 15^10 per factor, >= ~1e-2) -- which
 // halves the transcendental work of the NLL passes. Arguments: d_j + r >=
 // 1/101 - ... > 0 (r = 1/delta - 1 >= 1/0.99 - 1, pseudodata >= 0).
+// nll_pixel where every lgamma argument is >= 20 (r = 1/delta - 1 >= 20,
+// pseudodata >= 0, z + n r >= 2 r): no shift products, the 5-term Stirling
+// series (lgam_nll_large). The Brent kernels take it for the evaluations
+// whose r is that large -- the searches' trial points near the optimum at
+// the usual dispersions ~0.01..0.05 -- with a branch that is uniform across
+// the segment.
+template <int M>
+H3D_HD double nll_pixel_large(const double* d, int n, const NllConst& k,
+                              const LogTab* tab = kLogTab) {
+  double lg[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam_nll_large(d[j] + k.r, tab) : 0.0;
+  const double z = np_sum<M>(d, n);
+  const double lz = lgam_nll_large(z + k.nr, tab);
+  return np_sum<M>(lg, n) + k.lg_nr - lz - k.n_lg_r;
+}
+
+constexpr double kNllLargeR = 20.0;
+
 template <int M>
 H3D_HD double nll_pixel(const double* d, int n, const NllConst& k,
                         const LogTab* tab = kLogTab) {

@@ -457,6 +457,29 @@ H3D_HD double lgam_nll(double x) {
   return v;
 }
 
+// Stirling series of the NLL lgamma with the first 5 Bernoulli terms, for y
+// >= 20: the first omitted term, B12 / (12 11 y^11), is < 1e-17 there (the
+// 8-term series of stirling_nll is needed down to y = 10)
+H3D_HD double stirling_nll5(double r2) {
+  double q = 1.0 / 1188.0;
+  q = hfma(q, r2, -1.0 / 1680.0);
+  q = hfma(q, r2, 1.0 / 1260.0);
+  q = hfma(q, r2, -1.0 / 360.0);
+  return hfma(q, r2, 1.0 / 12.0);
+}
+
+// lgam_nll_parts for x >= 20 (the caller knows it for every lane: the NLL
+// arguments d + r with r >= 20, pseudodata d >= 0): no shift product (*P is
+// 1), the 5-term Stirling series. Same accuracy as lgam_nll_parts there.
+H3D_HD double lgam_nll_large(double x, const LogTab* tab = kLogTab) {
+#if defined(__clang__)
+#pragma clang fp contract(fast)
+#endif
+  const double r = recip_nll(x), r2 = r * r;
+  const double corr = r * stirling_nll5(r2);
+  return (x - 0.5) * log_fast(x, tab) - x + kLogSqrt2Pi + corr;
+}
+
 // lgam_nll split for batching: returns lgam(x) + ln P and sets *P, the
 // shift product (1 for x >= 10), so a caller summing several lgammas takes
 // ONE log of the combined product (nll_pixel: per pixel R_c + 1 lgammas, one

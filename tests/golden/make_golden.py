@@ -671,7 +671,7 @@ CFG1 = {'chr18': 9070, 'chr19': 6143}   # mm10 chr18 / chr19 at 10 kb
 
 
 def run_full_cfg1(dmax=200, seed=7, chunk=20000, n_sample=20000,
-                  fdrs=(0.01, 0.05), sizes=(3, 4)):
+                  fdrs=(0.01, 0.05), sizes=(3, 4), perm=0):
     """BASELINE configs[0]'s shape at full size (the Bonev demo's chr18 +
     chr19 at 10 kb, R = 4 as 2 + 2, dist_thresh_max 200; synthetic data of
     that shape, with loop clusters, since the demo data is not available
@@ -683,7 +683,9 @@ def run_full_cfg1(dmax=200, seed=7, chunk=20000, n_sample=20000,
     threshold, classify, the results TSV) at every (fdr, cluster size).
     full_cfg1.npz: disp_per_dist, per chromosome a seeded sample of disp
     pixels with p / llr / mu0 / mu1, every loop pixel's q, the call sets,
-    and the text of every results_<fdr>_<size>.tsv."""
+    and the text of every results_<fdr>_<size>.tsv. perm > 0: the same run
+    with every segment's pixels in a seeded permutation of their order
+    (_PermutedQcml; run_cfg1_spread), the dict returned, nothing written."""
     import multiprocessing
     # (the inputs are regenerated from the seed by the test, as full_cfg2's)
     base = os.path.join('/tmp', 'h3golden_cfg1_data')
@@ -697,7 +699,12 @@ def run_full_cfg1(dmax=200, seed=7, chunk=20000, n_sample=20000,
                   design=design, outdir=outdir, dist_thresh_max=dmax,
                   loop_patterns=kw['loop_patterns'], res=10000)
     h.prepare_data(n_threads=-1, verbose=False)
-    h.estimate_disp(n_threads=-1)
+    dispersion.__dict__.setdefault('_orig_qcml', dispersion.qcml)
+    dispersion.qcml = _PermutedQcml(perm)
+    try:
+        h.estimate_disp(n_threads=-1)
+    finally:
+        dispersion.qcml = dispersion.__dict__['_orig_qcml']
     dsg = design.values
     rng = np.random.default_rng(seed)
     out = {'meta_chroms': np.array(kw['chroms']),
@@ -742,12 +749,36 @@ def run_full_cfg1(dmax=200, seed=7, chunk=20000, n_sample=20000,
             with open(os.path.join(outdir, 'results_%g_%i.tsv' % (fdr, size))) \
                     as fh:
                 out['results_%g_%i' % (fdr, size)] = np.array(fh.read())
+    if perm:
+        return out
     np.savez_compressed(os.path.join(HERE, 'full_cfg1.npz'), **out)
     print('full cfg1:', {c: int(out['n_disp__%s' % c]) for c in kw['chroms']},
           'loop pixels', {c: int(out['loop_idx__%s' % c].sum())
                           for c in kw['chroms']},
           'results lines', {k: str(v).count('\n') for k, v in out.items()
                             if k.startswith('results_')})
+
+
+def run_cfg1_spread(perms=(1, 2, 3, 4, 5)):
+    """The reference's own spread on the cfg1 genome (run_full_cfg1 with
+    every segment's pixels permuted, as run_cfg2_spread): cfg1_spread.npz
+    holds per permutation k disp_per_dist__k, per chromosome p__<chrom>__k
+    (full_cfg1's sample pixels) and q__<chrom>__k (every loop pixel); the
+    unpermuted run is full_cfg1.npz itself (order 0)."""
+    g = np.load(os.path.join(HERE, 'full_cfg1.npz'))
+    chroms = [str(c) for c in g['meta_chroms']]
+    out = {'perms': np.array((0,) + tuple(perms))}
+    for k in perms:
+        o = run_full_cfg1(perm=k)
+        out['disp_per_dist__%d' % k] = o['disp_per_dist']
+        for c in chroms:
+            out['p__%s__%d' % (c, k)] = o['p__%s' % c]
+            out['q__%s__%d' % (c, k)] = o['q__%s' % c]
+        rel = [np.max(np.abs(o['p__%s' % c] - g['p__%s' % c]) / g['p__%s' % c])
+               for c in chroms]
+        print('cfg1 perm %d: sample p max rel vs order 0 %s' % (k, rel),
+              flush=True)
+    np.savez_compressed(os.path.join(HERE, 'cfg1_spread.npz'), **out)
 
 
 class _PermutedQcml(object):
@@ -865,7 +896,8 @@ def run_sim_scale(dmax=200, seed=11, sim_seed=42):
     them, then its simulate('ES') (analysis/simulation.py:22-144 ->
     util/simulation.py:70-204) with np.random.seed(sim_seed), serially (the
     stream is consumed chromosome by chromosome). sim_scale.npz: the
-    reference's disp_per_dist, the cluster labels, and per simulated
+    reference's disp_per_dist and its disp_fn at every integer distance, the
+    cluster labels, and per simulated
     replicate and chromosome the sha256 of its CSR arrays, nnz, the count
     sum and the first 2,000 stored counts (the matrices themselves are ~40 M
     entries)."""
@@ -891,6 +923,11 @@ def run_sim_scale(dmax=200, seed=11, sim_seed=42):
            'meta_dmax': np.array(dmax), 'meta_cond': np.array('ES'),
            'meta_chroms': np.array(kw['chroms']),
            'disp_per_dist': np.load(os.path.join(outdir, 'disp_per_dist.npy'))}
+    # the reference's fitted disp_fn at every integer distance (simulate
+    # evaluates it at the pixels' distances only, trend='dist')
+    for cond in kw['conds']:
+        out['disp_fn_table__%s' % cond] = h.load_disp_fn(cond)(
+            np.arange(dmax + 1))
     for chrom in kw['chroms']:
         out['labels__%s' % chrom] = np.loadtxt(
             os.path.join(simdir, 'labels_%s.txt' % chrom), dtype='U7')
@@ -1016,6 +1053,8 @@ if __name__ == '__main__':
         run_cfg2_spread()
     if 'full_cfg1' in which:
         run_full_cfg1()
+    if 'cfg1_spread' in which:
+        run_cfg1_spread()
     if 'sim_scale' in which:
         run_sim_scale()
     if 'sim' in which:

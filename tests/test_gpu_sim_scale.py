@@ -3,15 +3,17 @@ scale: three full-size mm10 chromosomes (chr1-3 at 10 kb, 53,753 bins, R =
 4 as 2 + 2, dist_thresh_max 200, loop clusters), regenerated from their
 seed.
 
-1. The product's prepare_data (GPU) and the REFERENCE's dispersion
-   function (tests/golden/sim_scale.npz: its disp_per_dist, smoothed by the
-   product's smoother, bit-equal to the reference's on that input) feed the
+1. The product's prepare_data (GPU) and the REFERENCE's fitted dispersion
+   function (tests/golden/sim_scale.npz: its disp_fn at every integer
+   distance -- simulate evaluates it at the pixels' distances only) feed the
    product's simulate('ES') (analysis/simulation.py:22-144,
    util/simulation.py:70-204) with the reference's seed: every simulated
    replicate of every chromosome is the reference's, count for count (sha256
    of the CSR arrays), and the cluster labels are identical. The reference's
-   own disp_fn isolates the sampler from estimate_disp, whose segments may
-   land elsewhere inside Brent's tolerance (test_gpu_scale.py).
+   own disp_fn isolates the sampler from estimate_disp (whose segments may
+   land elsewhere inside Brent's tolerance, test_gpu_scale.py) and from the
+   pinned weighted-lowess floor deviation (the product's
+   smallest weight is exactly 1), which the test reports.
 2. The GPU analysis of the simulated set (run_to_qvalues, the simulated
    replicates biased by their source replicates' bias vectors), timed, and
    evaluate() on its q-values against the oracle's evaluate (the reference's
@@ -67,6 +69,23 @@ def simulated():
         tables = _native.disp_tables(dpd)
         for c, cond in enumerate(design.columns):
             h.save_disp_fn(cond, DispFn(tables[:, c], dpd[:, c]))
+            ref = g['disp_fn_table__%s' % cond]
+            ours = DispFn(tables[:, c], dpd[:, c])(np.arange(dmax + 1.0))
+            print('%s: the product smoother on the reference disp_per_dist vs '
+                  'the reference disp_fn: max rel %.3g' % (
+                      cond, np.max(np.abs(ours - ref) / ref)))
+        ref_fn = g['disp_fn_table__ES']
+
+        def lookup(cond):
+            assert cond == 'ES'
+
+            def fn(x):
+                xi = np.asarray(x).astype(np.int64)
+                assert np.array_equal(xi, x)   # integer distances only
+                return ref_fn[xi]
+            return fn
+        # the reference's disp_fn values for the sampler (instance override)
+        h.load_disp_fn = lookup
         sim = os.path.join(tmp, 'sim')
         np.random.seed(int(g['meta_sim_seed']))
         t0 = time.perf_counter()

@@ -33,7 +33,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--bins', type=int, default=1500)
     ap.add_argument('--dmax', type=int, default=250)
-    ap.add_argument('--key', choices=('maxmin', 'maxmin8', 'minmax', 'summax', 'summin', 'total'), default='maxmin')
+    ap.add_argument('--key', choices=('maxmin', 'maxmin8', 'minmax', 'summax',
+                                      'summin', 'total', 'ratio', 'sumratio',
+                                      'maxratio'), default='maxmin')
     args = ap.parse_args()
     import oracle
     from hic3defdr_amd import synthetic
@@ -77,6 +79,21 @@ def main():
             order = np.lexsort((mx, sm, dist0))
         elif args.key == 'summin':
             order = np.lexsort((mn, sm, dist0))
+        elif args.key in ('ratio', 'sumratio', 'maxratio'):
+            # the replicates' normalized counts' log ratio (how far each
+            # replicate sits from the pixel's mean: the tail position the
+            # incomplete-gamma trip counts depend on), 4 bins per e-fold
+            fc = f0[:, cond == c]
+            nrm = (rc + 0.5) / fc
+            lr = np.log(nrm.max(1) / nrm.min(1))
+            rcode = np.minimum((lr * 4).astype(np.int64), 63)
+
+            def code(v):
+                v = np.asarray(v, dtype=np.int64)
+                return np.where(v < 128, v, np.minimum(128 + (v - 128) // 8, 255))
+            lead = {'ratio': code(rc.min(1)), 'sumratio': code(rc.sum(1)),
+                    'maxratio': code(rc.max(1))}[args.key]
+            order = np.lexsort((rcode, lead, dist0))
         elif args.key == 'maxmin8':
             # 8-bit count codes: exact below 128, then 8 counts per code up
             # to 1151 (k_dist_cond_keys' compressed key)
