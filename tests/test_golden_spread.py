@@ -41,3 +41,20 @@ def test_reference_order_spread_fixture():
         for fdr in (0.01, 0.05, 0.1):
             np.testing.assert_array_equal(o['calls_%g' % fdr],
                                           g['calls_%g' % fdr])
+
+
+def test_cfg1_reference_order_spread_fixture():
+    """The same on the cfg1 genome (two chromosomes, loop-pixel BH;
+    cfg1_spread.npz, make_golden.py run_cfg1_spread): orders 1..5 of the
+    reference's segments against its order 0 (full_cfg1.npz) move the
+    sampled p-values by 1e-9 .. 4.3e-3 -- again the reference's own spread
+    that test_gpu_cfg1.py's end-to-end bar is measured against."""
+    g = golden('full_cfg1.npz')
+    sp = golden('cfg1_spread.npz')
+    chroms = [str(c) for c in g['meta_chroms']]
+    spread = [max(rel_err(sp['p__%s__%d' % (c, k)], g['p__%s' % c])
+                  for c in chroms) for k in sp['perms'][1:]]
+    assert min(spread) < 1e-7 and 1e-4 < max(spread) < 1e-2, spread
+    for k in sp['perms'][1:]:
+        for c in chroms:
+            assert sp['q__%s__%d' % (c, k)].shape == g['q__%s' % c].shape

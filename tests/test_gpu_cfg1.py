@@ -70,28 +70,54 @@ def test_cfg1_disp_per_dist_vs_reference(cfg1):
     assert dd.max() <= 1e-5
 
 
+def _reference_orders(g):
+    """The reference's end-to-end p / q under six pixel orders of its
+    segments: order 0 = full_cfg1.npz, 1..5 = cfg1_spread.npz (make_golden.py
+    run_cfg1_spread). Measured: it moves itself by up to 4.3e-3 in p."""
+    sp = golden('cfg1_spread.npz')
+    out = [{c: (g['p__%s' % c], g['q__%s' % c]) for c in CFG1}]
+    for k in sp['perms'][1:]:
+        out.append({c: (sp['p__%s__%d' % (c, k)], sp['q__%s__%d' % (c, k)])
+                    for c in CFG1})
+    return out
+
+
 def test_cfg1_stages_vs_reference(cfg1):
+    """Per chromosome: disp pixel and loop sets identical; the sampled p and
+    every loop pixel's q within 1e-6 of the reference's end-to-end result
+    under one of its pixel orders (measured r04b: the product's p equal the
+    reference's orders 4 / 5 to ~1e-9 while those move 7.8e-5 from its
+    order 0); the mean MLEs within 1e-4 of order 0 (they see the segment
+    moves through disp); identical calls at q < 0.01 / 0.05 / 0.1."""
     h, g = cfg1
+    orders = _reference_orders(g)
+    ours = {}
     for chrom in CFG1:
         assert int(h.load_data('disp_idx', chrom).sum()) == \
             int(g['n_disp__%s' % chrom])
-        s = g['sample_idx__%s' % chrom]
-        p = h.load_data('pvalues', chrom)[s]
-        m0 = h.load_data('mu_hat_null', chrom)[s]
-        m1 = h.load_data('mu_hat_alt', chrom)[s]
-        e = (rel_err(p, g['p__%s' % chrom]),
-             rel_err(m0, g['mu0__%s' % chrom]),
-             rel_err(m1, g['mu1__%s' % chrom]))
-        print('cfg1 %s: sample p rel %.3g, mu0 %.3g, mu1 %.3g' % ((chrom,) + e))
-        assert max(e) < 1e-5
         np.testing.assert_array_equal(h.load_data('loop_idx', chrom),
                                       g['loop_idx__%s' % chrom])
-        q = h.load_data('qvalues', chrom)
-        print('cfg1 %s: %d loop-pixel q, max rel %.3g' % (
-            chrom, len(q), rel_err(q, g['q__%s' % chrom])))
-        assert rel_err(q, g['q__%s' % chrom]) < 1e-5
+        s = g['sample_idx__%s' % chrom]
+        ours[chrom] = (h.load_data('pvalues', chrom)[s],
+                       h.load_data('qvalues', chrom))
+        m0 = h.load_data('mu_hat_null', chrom)[s]
+        m1 = h.load_data('mu_hat_alt', chrom)[s]
+        e0 = (rel_err(ours[chrom][0], g['p__%s' % chrom]),
+              rel_err(ours[chrom][1], g['q__%s' % chrom]),
+              rel_err(m0, g['mu0__%s' % chrom]),
+              rel_err(m1, g['mu1__%s' % chrom]))
+        print('cfg1 %s vs the reference: sample p rel %.3g, loop q rel %.3g, '
+              'mu0 %.3g, mu1 %.3g' % ((chrom,) + e0))
+        assert max(e0[2:]) < 1e-4
         for fdr in (0.01, 0.05, 0.1):
-            np.testing.assert_array_equal(q < fdr, g['q__%s' % chrom] < fdr)
+            np.testing.assert_array_equal(ours[chrom][1] < fdr,
+                                          g['q__%s' % chrom] < fdr)
+    near = [max(max(rel_err(ours[c][0], o[c][0]), rel_err(ours[c][1], o[c][1]))
+                for c in CFG1) for o in orders]
+    k = int(np.argmin(near))
+    print('cfg1: p / q vs each reference order %s; nearest %d' % (
+        ['%.2g' % v for v in near], k))
+    assert near[k] < 1e-6
 
 
 def _rows(text):
