@@ -97,13 +97,12 @@ struct NpSumStream {
 // The reference finds it with scipy's array secant + a brentq fallback
 // (scaled_nb.py:149-181). The log-likelihood is strictly concave in
 // theta = log(mu), so the root is unique; here it is found per lane by
-// Newton on g(theta) = mu S(mu) inside a shrinking bracket (bisection
+// Halley steps on g(theta) = mu S(mu) inside a shrinking bracket (bisection
 // safeguard), to full double precision.
 template <int M, typename TX>
 H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
                      unsigned mask, int* status) {
-  double sx = 0.0, init = 0.0;
-  int cnt = 0;
+  double sx = 0.0, sb = 0.0;
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < M; ++k)
@@ -111,8 +110,7 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
       bad |= !(a[k] > 0.0) || !(b[k] > 0.0) || is_inf(a[k]) || is_inf(b[k]) ||
              !(x[k] >= 0.0);
       sx += x[k];
-      init += x[k] / b[k];
-      ++cnt;
+      sb += b[k];
     }
   if (bad) {
     *status |= kFlagBadInput;
@@ -123,23 +121,31 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
     return NAN;
   }
   H3D_STAT(fit, 1);
+  // start at sum(x) / sum(b), the MLE of the Poisson limit (alpha -> 0),
+  // instead of the reference's secant start mean(x / b) (scaled_nb.py:150):
+  // the root is unique and converged to full precision either way, and this
+  // start is closer to it (wave of 64 pixels: 2.37 against 2.62 steps)
   // (the table log and straight-line exp of h3d_special.h: ~1 ulp, the
   // OCML forms carried constant copies; the MLE is Newton-converged anyway)
-  double th = log_fast_checked(init / cnt);
+  double th = log_fast_checked(div_fast(sx, sb));
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
     H3D_STAT(fit_it, 1);
     const double mu = exp_fast(th);
-    double g = 0.0, gp = 0.0;
+    double g = 0.0, gp = 0.0, gpp = 0.0;
 #pragma unroll
     for (int k = 0; k < M; ++k)
       if (k < n && ((mask >> k) & 1u)) {
         const double mb = mu * b[k];
+        const double am = a[k] * mb;
         // v_rcp_f64 + one Newton step on gfx950 (the IEEE division sequence
         // was ~12 VALU per replicate and iteration)
-        const double den = recip_fast(1.0 + a[k] * mb);
+        const double den = recip_fast(1.0 + am);
         g += (x[k] - mb) * den;
-        gp -= mb * (1.0 + a[k] * x[k]) * den * den;
+        // g' and g'' in theta: d(mb)/dtheta = mb, d(den)/dtheta = -am den^2
+        const double t = mb * (1.0 + a[k] * x[k]) * den * den;
+        gp -= t;
+        gpp -= t * (1.0 - 2.0 * am * den);
       }
     if (g > 0.0)
       lo = th;
@@ -147,12 +153,18 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
       hi = th;
     else
       return mu;
-    const double dn = g * recip_fast(gp);
-    // Newton converges quadratically here (g is smooth and monotone in
-    // theta): once a step is <= 1e-8 the error after it is ~1e-16, so take
-    // it and stop. (Without this exit, a final step below one ulp left th
-    // on the bracket edge and fell through to ~50 bisections.)
-    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
+    // Halley's step g / (g' - g g'' / (2 g')), the Newton step where the
+    // correction factor is far from 1 (away from the root; the bracket below
+    // catches what is left). Near the root it converges cubically: once a
+    // step is <= 1e-5 the error after it is ~1e-15, so take it and stop
+    // (2.0 steps per fit on average, 2.4 per wave of 64 pixels against 3.5
+    // for Newton with its 1e-8 exit, tools census r04). (Without an exit of
+    // this kind, a final step below one ulp left th on the bracket edge and
+    // fell through to ~50 bisections.)
+    const double nt = g * recip_fast(gp);
+    const double hf = 1.0 - 0.5 * nt * gpp * recip_fast(gp);
+    const double dn = (hf >= 0.5 && hf <= 2.0) ? nt * recip_fast(hf) : nt;
+    if (fabs(dn) <= 1e-5 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
     double tn = th - dn;
     if (!(tn > lo && tn < hi)) {
       if (is_inf(lo))

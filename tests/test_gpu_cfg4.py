@@ -73,6 +73,8 @@ def test_cfg4_full_chromosome(cfg4):
             rel.append(abs(got - want) / abs(want))
             ddelta.append(abs(got / (1 + got) - want / (1 + want)))
     rel, ddelta = np.array(rel), np.array(ddelta)
+    print('cfg4 segments vs the oracle: rel %s, |d delta| %s' % (
+        np.array2string(rel, precision=2), np.array2string(ddelta, precision=2)))
     assert (rel <= 1e-6).sum() >= len(rel) - 1, rel
     assert np.all(ddelta <= 2e-5), ddelta
 

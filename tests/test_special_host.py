@@ -128,6 +128,37 @@ def test_fit_mu_vs_goldens(lib):
         assert rel_err(mu, ref) < 1e-9
 
 
+def test_fit_mu_is_converged_to_full_precision(lib):
+    """fit_mu's Halley steps stop once a step is <= 1e-5 in log mu (cubic
+    convergence: ~1e-15 after it). The root of the score S(mu)
+    (scaled_nb.py:143-147) must lie within 1e-12 relative of the returned
+    mu, over counts from 0 to 1e5, dispersions 1e-6 .. 10 and size factors
+    1e-3 .. 1e3 (some replicates zero)."""
+    rng = np.random.default_rng(5)
+    n = 40000
+    lam = 10 ** rng.uniform(-1, 5, (n, 1))
+    b = 10 ** rng.uniform(-1.5, 1.5, (n, 4)) * 10 ** rng.uniform(-1.5, 1.5, (n, 1))
+    al = 10 ** rng.uniform(-6, 1, (n, 4))
+    x = rng.poisson(lam * b).astype(np.int32)
+    x[rng.random((n, 4)) < 0.1] = 0
+    x[x.sum(1) == 0, 0] = 1
+    mu = np.empty(n)
+    st = lib.h3dt_fit_mu(ctypes.c_int64(n), 4, _p(x, I), _p(b), _p(al), _p(mu))
+    assert st == 0 and np.all(mu > 0)
+    # a pixel whose only non-zero replicate has a far smaller dispersion
+    # than the zero ones can have S > 0 for every mu (the MLE at infinity)
+    fin = np.isfinite(mu)
+    assert fin.sum() >= n - 5
+    x, b, al, mu = x[fin], b[fin], al[fin], mu[fin]
+
+    def score(m):
+        mb = m[:, None] * b
+        return ((x - mb) / (m[:, None] + al * m[:, None] * mb)).sum(1)
+    lo, hi = score(mu * (1 - 1e-12)), score(mu * (1 + 1e-12))
+    # S decreases through the root: S(mu (1 - eps)) >= 0 >= S(mu (1 + eps))
+    assert np.all(lo >= 0) and np.all(hi <= 0)
+
+
 def test_fit_mu_doctest_brentq_case(lib):
     """scaled_nb.py:129-137: the second pixel needs the brentq fallback."""
     x = np.array([[2, 3, 4, 2], [6, 9, 3, 1]], dtype=np.int32)

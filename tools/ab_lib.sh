@@ -14,6 +14,6 @@ for v in $vs; do
   python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').read().splitlines()[-1]); k=d['kernels_ms_per_step']; print('$v', round(d['value']/1e6,1), round(d['ms_per_step'],3), {a: round(b,3) for a, b in k.items() if a != 'note'})"
 done
 done
-H3D_LIB=$PWD/hic3defdr_amd/lib/variants/libh3d_$first.so timeout -k 10 600 python3 -u -m pytest tests -m gpu -q --timeout 300 \
+H3D_LIB=$PWD/hic3defdr_amd/lib/variants/libh3d_$first.so timeout -k 10 600 python3 -u -m pytest tests -m gpu -q -rP --timeout 300 \
   --timeout-method thread > gpurun_out/ab_gpu_tests.log 2>&1 || { tail -n 40 gpurun_out/ab_gpu_tests.log; exit 1; }
 tail -n 2 gpurun_out/ab_gpu_tests.log

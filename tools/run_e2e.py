@@ -1,0 +1,140 @@
+"""BASELINE configs[2] (cfg3, the mouse genome at 10 kb: 20 chromosomes,
+~263k bins, R = 4 as 2 + 2, dist_thresh_max 200) END TO END through the
+product class, files included: the synthetic genome is written in the
+reference's input layout (per-replicate NPZ + bias files, loop-cluster
+JSON; synthetic.py's generator, each chromosome from its own seed, written
+by a process pool), then ``HiC3DeFDR.run_to_qvalues()`` (prepare_data ->
+estimate_disp -> lrt -> bh, analysis.py:305-364 of the reference) and
+``collect()`` run on it, each stage timed; the outdir writes land behind the
+stages (write-behind) and the wait for the last of them is reported.
+
+    python tools/run_e2e.py [--chroms 20] [--workers 16] [--keep DIR]
+
+Prints one JSON line. Under torchrun it runs the sharded path (each rank
+its LPT chromosomes, the distance re-shard, the sample-sort BH).
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+DMAX = 200
+
+
+def _write_chrom(args):
+    import scipy.sparse as sp
+    from hic3defdr_amd import synthetic
+    base, i, n_bins, seed = args
+    chrom = 'chr%d' % (i + 1)
+    reps, conds, design = synthetic.default_design((2, 2))
+    rng = np.random.default_rng([seed, i])
+    mats, bias = synthetic.generate_chrom(rng, n_bins, DMAX + 50, design)
+    for k, rep in enumerate(reps):
+        sp.save_npz(os.path.join(base, rep, '%s_raw.npz' % chrom), mats[k])
+        np.savetxt(os.path.join(base, rep, '%s_kr.bias' % chrom), bias[:, k])
+    for cond in conds:
+        cl = synthetic.generate_clusters(rng, n_bins, DMAX, max(3, n_bins // 50))
+        with open(os.path.join(base, 'clusters', '%s_%s.json' % (cond, chrom)),
+                  'w') as fh:
+            json.dump(cl, fh)
+    return chrom
+
+
+def write_genome(base, bins, seed, workers):
+    from hic3defdr_amd import synthetic
+    reps, conds, design = synthetic.default_design((2, 2))
+    for rep in reps:
+        os.makedirs(os.path.join(base, rep), exist_ok=True)
+    os.makedirs(os.path.join(base, 'clusters'), exist_ok=True)
+    # largest chromosomes first so the pool's tail is short
+    order = sorted(range(len(bins)), key=lambda i: -bins[i])
+    with ProcessPoolExecutor(workers) as ex:
+        list(ex.map(_write_chrom, [(base, i, bins[i], seed) for i in order]))
+    chroms = ['chr%d' % (i + 1) for i in range(len(bins))]
+    return dict(
+        raw_npz_patterns=[os.path.join(base, r, '<chrom>_raw.npz') for r in reps],
+        bias_patterns=[os.path.join(base, r, '<chrom>_kr.bias') for r in reps],
+        chroms=chroms, reps=reps, conds=conds, design=design,
+        loop_patterns={c: os.path.join(base, 'clusters', '%s_<chrom>.json' % c)
+                       for c in conds})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--chroms', type=int, default=20)
+    ap.add_argument('--workers', type=int, default=16)
+    ap.add_argument('--seed', type=int, default=3)
+    ap.add_argument('--keep', default=None,
+                    help='write the dataset and outdir here and keep them')
+    args = ap.parse_args()
+    import pandas as pd
+    from hic3defdr_amd import HiC3DeFDR
+    from hic3defdr_amd.synthetic import MM10_BINS
+    bins = list(MM10_BINS[:args.chroms])
+    base = args.keep or tempfile.mkdtemp(prefix='h3d_e2e_')
+    os.makedirs(base, exist_ok=True)
+    try:
+        t0 = time.perf_counter()
+        kw = write_genome(base, bins, args.seed, args.workers)
+        write_s = time.perf_counter() - t0
+        print('genome written: %d chromosomes, %d bins, %.1f s' % (
+            len(bins), sum(bins), write_s), file=sys.stderr, flush=True)
+        design = pd.DataFrame(kw['design'], index=kw['reps'],
+                              columns=kw['conds'])
+        h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                      bias_patterns=kw['bias_patterns'], chroms=kw['chroms'],
+                      design=design, outdir=os.path.join(base, 'out'),
+                      dist_thresh_max=DMAX, loop_patterns=kw['loop_patterns'],
+                      res=10000)
+        stages = {}
+        t = time.perf_counter()
+        for name, fn in (('prepare_data', lambda: h.prepare_data(verbose=False)),
+                         ('estimate_disp', h.estimate_disp),
+                         ('lrt', lambda: h.lrt(verbose=False)),
+                         ('bh', h.bh),
+                         ('outdir_flush', h.flush)):
+            fn()
+            now = time.perf_counter()
+            stages[name + '_s'] = now - t
+            t = now
+            print('  %s %.3f s' % (name, stages[name + '_s']), file=sys.stderr,
+                  flush=True)
+        total = sum(stages.values())
+        t = time.perf_counter()
+        h.collect(fdr=[0.01, 0.05], cluster_size=[3, 4])
+        h.flush()
+        collect_s = time.perf_counter() - t
+        sh = h._shards()
+        n_disp = sum(int(h.load_data('disp_idx', c).sum()) for c in sh.mine)
+        q = np.concatenate([h.load_data('qvalues', c) for c in sh.mine]) \
+            if sh.mine else np.zeros(0)
+        out = {
+            'config': 'cfg3 end to end (files)', 'chroms': len(bins),
+            'bins': int(sum(bins)), 'reps': 4, 'conds': 2,
+            'dist_thresh_max': DMAX, 'rank': sh.rank, 'world': sh.world,
+            'disp_pixels_this_rank': n_disp,
+            'run_to_qvalues_s': total, 'stages': stages,
+            'pixels_per_s_run_to_qvalues': n_disp / total,
+            'estimate_disp_plus_lrt_s': stages['estimate_disp_s'] +
+            stages['lrt_s'],
+            'collect_s': collect_s, 'write_dataset_s': write_s,
+            'loop_pixels_q_lt_0.05': int(np.sum(q < 0.05)),
+        }
+        if sh.rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
+        if not args.keep:
+            shutil.rmtree(base, ignore_errors=True)
+
+
+if __name__ == '__main__':
+    main()
