@@ -34,6 +34,7 @@ EXPORTS = [
     'h3d_estimate_disp_dev', 'h3d_bh_sort_dev', 'h3d_bh_scan_dev',
     'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
     'h3d_disp_pixels_dev', 'h3d_table_gather_dev', 'h3d_disp_seg_stats',
+    'h3d_scale_disp_dev',
 ]
 
 
@@ -96,6 +97,8 @@ def load_library(path=None):
             'h3d_disp_pixels_dev': (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _P,
                                          _I64, _I, _I64, _P, _P, _P]),
             'h3d_table_gather_dev': (_I, [_P, _P, _I, _I, _P, _I64, _P]),
+            'h3d_scale_disp_dev': (_I, [_P, _P, _P, _I, _P, _P, _I64, _I, _I,
+                                        _P, ctypes.c_double, _I, _P, _P, _P]),
             'h3d_disp_seg_stats': (_I, [_P, _I, _P, _P]),
             'h3d_size_factors_cmor': (_I, [_P, _P, _P, _I64, _I, _I, _P]),
             'h3d_size_factors': (_I, [_P, _P, _P, _I64, _I, _I, _I, _P]),
@@ -235,13 +238,16 @@ class Context(object):
                'h3d_set_stream')
 
     # -- prepare_data -------------------------------------------------------
-    def sparse_union(self, csrs, bias, dist_max, device_alloc=None):
+    def sparse_union(self, csrs, bias, dist_max, device_alloc=None,
+                     host_balanced=True):
         """csrs: list of canonical CSR matrices (scipy or `CSR`, n_bins x
         n_bins); bias
         (n_bins, R) filtered. Returns row, col (int32), raw (int64 (n, R)),
         balanced (float64 (n, R)). ``device_alloc(n, R)``, when given,
         returns device pointers (row, col, raw int32, balanced; any may be
-        None) that also receive the union (h3d_union_fill_dev)."""
+        None) that also receive the union (h3d_union_fill_dev); with a device
+        balanced, ``host_balanced=False`` skips its host copy (balanced is
+        then None)."""
         R = len(csrs)
         n_bins = bias.shape[0]
         keep = []
@@ -265,15 +271,19 @@ class Context(object):
         row = np.empty(n, dtype=np.int32)
         col = np.empty(n, dtype=np.int32)
         raw = np.empty((n, R), dtype=np.int64)
-        bal = np.empty((n, R), dtype=np.float64)
+        bal = np.empty((n, R), dtype=np.float64) \
+            if host_balanced or device_alloc is None else None
         if device_alloc is None:
             _check(self.lib.h3d_union_fill(self.handle, _ptr(row), _ptr(col),
                                            _ptr(raw), _ptr(bal), n),
                    'h3d_union_fill')
         else:
             d = device_alloc(n, R)
+            if bal is None and n and not d[3]:
+                raise ValueError('host_balanced=False needs a device balanced')
             _check(self.lib.h3d_union_fill_dev(
-                self.handle, _ptr(row), _ptr(col), _ptr(raw), _ptr(bal), n,
+                self.handle, _ptr(row), _ptr(col), _ptr(raw),
+                _ptr(bal) if bal is not None else None, n,
                 *[_P(v) if v else None for v in d]), 'h3d_union_fill_dev')
         return row, col, raw, bal
 
@@ -291,6 +301,25 @@ class Context(object):
             int(n_bins or 0), _ptr(out), _P(d_sf_out) if d_sf_out else None),
             'h3d_size_factors_dev')
         return out
+
+    def scale_disp_dev(self, d_balanced, d_sf, sf_per_rep, d_row, d_col, n,
+                       R, design, mean_thresh, dist_thresh_min,
+                       d_flag_out=None):
+        """prepare_data's scaled (n, R) and disp_idx flags (n; 0 / 1, or 2
+        where numpy's product decides) on the device (h3d_scale_disp_dev);
+        returns the host copies (scaled, flag)."""
+        design = np.ascontiguousarray(design, dtype=np.uint8)
+        if design.ndim != 2 or design.shape[0] != R:
+            raise ValueError('design must be (R, C)')
+        scaled = np.empty((n, R), dtype=np.float64)
+        flag = np.empty(n, dtype=np.uint8)
+        _check(self.lib.h3d_scale_disp_dev(
+            self.handle, _P(d_balanced), _P(d_sf), int(bool(sf_per_rep)),
+            _P(d_row), _P(d_col), n, R, design.shape[1], _ptr(design),
+            float(mean_thresh), int(dist_thresh_min), _ptr(scaled),
+            _ptr(flag), _P(d_flag_out) if d_flag_out else None),
+            'h3d_scale_disp_dev')
+        return scaled, flag
 
     def disp_pixels_dev(self, d_row, d_col, d_raw, d_sf, sf_per_rep, bias,
                         d_disp_idx, n, R, n_disp, d_raw_out, d_f_out,

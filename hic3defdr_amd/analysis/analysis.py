@@ -122,7 +122,8 @@ class AnalyzingHiC3DeFDR(object):
         try:
             row, col, raw, balanced = ctx.sparse_union(
                 mats, bias, self.dist_thresh_max,
-                device_alloc=res.union_alloc(holder) if res else None)
+                device_alloc=res.union_alloc(holder) if res else None,
+                host_balanced=res is None)
         except _native.H3DError:
             if not holder:
                 raise
@@ -133,16 +134,19 @@ class AnalyzingHiC3DeFDR(object):
                                                        self.dist_thresh_max)
         eprint('  computing size factors', skip=not verbose)
         dist = col - row
+        design = np.asarray(self.design, dtype=bool)
         # analysis.py:104-108: conditional norms see the distances
         if res is not None and 'bal' in holder:
             size_factors = res.size_factors(holder, dist, norm, n_bins or 0)
+            # analysis.py:109-115 on the device (h3d_scale_disp_dev)
+            scaled, disp_idx = res.scale_disp(holder, design, self.mean_thresh,
+                                              self.dist_thresh_min, dist)
         else:
             size_factors = ctx.size_factors(balanced, dist, norm, n_bins or 0)
-        scaled = balanced / size_factors
-        design = np.asarray(self.design, dtype=bool)
-        mean = np.dot(scaled, design) / np.sum(design, axis=0)
-        disp_idx = np.all(mean >= self.mean_thresh, axis=1) & \
-            (dist >= self.dist_thresh_min)
+            scaled = balanced / size_factors
+            mean = np.dot(scaled, design) / np.sum(design, axis=0)
+            disp_idx = np.all(mean >= self.mean_thresh, axis=1) & \
+                (dist >= self.dist_thresh_min)
         if self.loop_patterns:
             eprint('  making loop_idx', skip=not verbose)
             cl = [load_clusters(p.replace('<chrom>', chrom))

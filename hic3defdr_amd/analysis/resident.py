@@ -119,15 +119,44 @@ class Resident(object):
         sf = self.ctx.size_factors_dev(
             holder['bal'].data_ptr() if n else None, dist, n, R, norm, n_bins,
             d_sf_out=holder['sf'].data_ptr() if holder['sf'].numel() else None)
-        del holder['bal']
         return sf
+
+    def scale_disp(self, holder, design, mean_thresh, dist_min, dist):
+        """scaled and disp_idx (analysis.py:109-115) from the resident
+        balanced and size factors (h3d_scale_disp_dev); the disp flags stay
+        on the device in ``holder['di']``, balanced is released. The rows the
+        device leaves to numpy's product (flag 2: non-finite, or a mean
+        within 1e-12 of the threshold) are decided here by the reference's
+        own expression."""
+        torch = self.torch
+        n, R = holder['bal'].shape
+        holder['di'] = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        sf = holder['sf']
+        scaled, flag = self.ctx.scale_disp_dev(
+            holder['bal'].data_ptr() if n else None,
+            sf.data_ptr() if sf.numel() else None, sf.dim() == 1,
+            holder['row'].data_ptr() if n else None,
+            holder['col'].data_ptr() if n else None, n, R, design,
+            mean_thresh, dist_min,
+            d_flag_out=holder['di'].data_ptr() if n else None)
+        del holder['bal']
+        disp_idx = flag == 1
+        amb = np.flatnonzero(flag == 2)
+        if len(amb):
+            mean = np.dot(scaled[amb], design) / np.sum(design, axis=0)
+            disp_idx[amb] = np.all(mean >= mean_thresh, axis=1) & \
+                (dist[amb] >= dist_min)
+            holder['di'].copy_(torch.from_numpy(disp_idx.view(np.uint8)))
+        return scaled, disp_idx
 
     def keep(self, chrom, holder, disp_idx, bias):
         """Registers a prepared chromosome (its stage files just queued)."""
         torch = self.torch
         n = int(holder['row'].shape[0])
-        t_di = torch.from_numpy(np.ascontiguousarray(
-            disp_idx, dtype=np.uint8)).to(self.dev)
+        t_di = holder.get('di')
+        if t_di is None:
+            t_di = torch.from_numpy(np.ascontiguousarray(
+                disp_idx, dtype=np.uint8)).to(self.dev)
         files = {self.h._npy(s, chrom): ('ours', self.h.write_generation(
             self.h._npy(s, chrom))) for s in self.STAGES}
         files.update(self._bias_stamps(chrom))

@@ -386,6 +386,55 @@ static __global__ void k_disp_pixels(const int32_t* __restrict__ sel, int64_t n_
   }
 }
 
+// prepare_data's scaled and disp_idx (analysis.py:109-115):
+//   scaled = balanced / size_factors,
+//   mean = np.dot(scaled, design) / n_c,
+//   disp_idx = all(mean >= mean_thresh, axis=1) & (dist >= dist_thresh_min).
+// The product is summed over every replicate in order with the design's 0 / 1
+// weights (a weight-0 term adds s * 0: 0, or NaN for an infinite s, as in the
+// BLAS product). A row whose decision could depend on the product's
+// summation order -- a non-finite scaled value, or a condition mean within
+// 1e-12 relative of the threshold -- is flagged 2, and the host decides it
+// with numpy's own product (h3d_scale_disp_dev). scaled goes out (n, R);
+// flag (n) is 0 / 1 / 2.
+struct ScaleDispArgs {
+  uint32_t cond_mask[kMaxConds];  // replicate bits of each condition
+  double count[kMaxConds];        // replicates per condition (the divisor)
+  int C;
+  double mean_thresh;
+  int dist_min;
+};
+
+static __global__ void k_scale_disp(const double* __restrict__ bal,
+                                    const double* __restrict__ sf, int sf_per_rep,
+                                    const int32_t* __restrict__ row,
+                                    const int32_t* __restrict__ col, int64_t n, int R,
+                                    ScaleDispArgs a, double* __restrict__ scaled,
+                                    uint8_t* __restrict__ flag) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    bool near = false;
+    for (int k = 0; k < R; ++k) {
+      const double v = bal[i * R + k] / (sf_per_rep ? sf[k] : sf[i * R + k]);
+      scaled[i * R + k] = v;
+      near |= !isfinite(v);
+    }
+    bool keep = (col[i] - row[i]) >= a.dist_min;
+    for (int c = 0; c < a.C; ++c) {
+      double acc = 0.0;
+      for (int k = 0; k < R; ++k) {
+        // the same IEEE quotient as above (re-derived, not re-read)
+        const double v = bal[i * R + k] / (sf_per_rep ? sf[k] : sf[i * R + k]);
+        acc += ((a.cond_mask[c] >> k) & 1u) ? v : v * 0.0;
+      }
+      const double mean = acc / a.count[c];
+      keep &= mean >= a.mean_thresh;
+      near |= fabs(mean - a.mean_thresh) <= 1e-12 * fabs(a.mean_thresh);
+    }
+    flag[i] = near ? 2 : (keep ? 1 : 0);
+  }
+}
+
 // disp[i, c] = table[dist[i], c] (analysis.py:218 disp_fn(dist): the fitted
 // function evaluated at integer distances IS its tabulation); NaN outside
 // [0, D)

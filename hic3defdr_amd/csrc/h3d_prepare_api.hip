@@ -169,7 +169,7 @@ int h3d_union_fill_dev(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
   PrepUnion& P = ctx->prep;
   if (n_px != P.n_px) return fail(H3D_EARG, "n_px %lld != counted %lld", (long long)n_px, (long long)P.n_px);
   if (n_px == 0) return 0;
-  if (!row || !col || !raw || !balanced) return fail(H3D_EARG, "null output");
+  if (!row || !col || !raw || (!balanced && !d_bal_out)) return fail(H3D_EARG, "null output");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   const int R = P.R;
@@ -200,7 +200,8 @@ int h3d_union_fill_dev(h3d_ctx* ctx, int32_t* row, int32_t* col, int64_t* raw,
   HIP_TRY(hipMemcpyAsync(row, d_row, n_px * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(col, d_col, n_px * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(raw, d_raw, n_px * R * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(balanced, d_bal, n_px * R * 8, hipMemcpyDeviceToHost, s));
+  if (balanced)
+    HIP_TRY(hipMemcpyAsync(balanced, d_bal, n_px * R * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (ovf) return fail(H3D_EINPUT, "raw counts must be in [0, 2^31) for the device copy");
   return 0;
@@ -246,6 +247,45 @@ int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col
                      n_disp, d_row, d_col, d_raw, d_sf, sf_per_rep, d_bias, R, d_raw_out,
                      d_f_out, d_dist_out);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int h3d_scale_disp_dev(h3d_ctx* ctx, const double* d_balanced, const double* d_sf,
+                       int sf_per_rep, const int32_t* d_row, const int32_t* d_col, int64_t n,
+                       int R, int C, const uint8_t* design, double mean_thresh,
+                       int dist_thresh_min, double* scaled_out, uint8_t* flag_out,
+                       uint8_t* d_flag_out) {
+  if (!ctx || !design) return fail(H3D_EARG, "null argument");
+  if (R < 1 || R > kMaxReps || C < 1 || C > kMaxConds || n < 0)
+    return fail(H3D_EARG, "R=%d C=%d n=%lld", R, C, (long long)n);
+  if (n == 0) return 0;
+  if (!d_balanced || !d_sf || !d_row || !d_col) return fail(H3D_EARG, "null device input");
+  if (!scaled_out || !flag_out) return fail(H3D_EARG, "null output");
+  ScaleDispArgs a{};
+  for (int c = 0; c < C; ++c) {
+    int cnt = 0;
+    for (int k = 0; k < R; ++k)
+      if (design[k * C + c]) {
+        a.cond_mask[c] |= 1u << k;
+        ++cnt;
+      }
+    // np.sum(design, axis=0): a condition without replicates divides by 0
+    a.count[c] = (double)cnt;
+  }
+  a.C = C;
+  a.mean_thresh = mean_thresh;
+  a.dist_min = dist_thresh_min;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  double* d_scaled = (double*)scratch(ctx, "sd_scaled", (size_t)n * R * 8);
+  uint8_t* d_flag = d_flag_out ? d_flag_out : (uint8_t*)scratch(ctx, "sd_flag", (size_t)n);
+  if (!d_scaled || !d_flag) return fail(H3D_ENOMEM, "scale / disp scratch");
+  hipLaunchKernelGGL(k_scale_disp, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_balanced,
+                     d_sf, sf_per_rep, d_row, d_col, n, R, a, d_scaled, d_flag);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(scaled_out, d_scaled, (size_t)n * R * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(flag_out, d_flag, (size_t)n, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return 0;
 }

@@ -198,4 +198,15 @@ def pixel_in(row, col, prow, pcol):
     prow = np.asarray(prow, dtype=np.int64)
     pcol = np.asarray(pcol, dtype=np.int64)
     base = int(max(pcol.max(), col.max())) + 1
-    return np.isin(row * base + col, prow * base + pcol)
+    keys = row * base + col
+    pk = prow * base + pcol
+    if len(keys) > 1 and not np.all(keys[1:] > keys[:-1]):
+        return np.isin(keys, pk)
+    # the union's pixels come in (row, col) order with unique keys: each set
+    # pixel is found by binary search (no sort of the chromosome's keys)
+    out = np.zeros(len(keys), dtype=bool)
+    pos = np.searchsorted(keys, pk)
+    ok = pos < len(keys)
+    pos, pk = pos[ok], pk[ok]
+    out[pos[keys[pos] == pk]] = True
+    return out

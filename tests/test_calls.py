@@ -192,3 +192,28 @@ def test_collect_needs_res():
             h.collect()
     finally:
         shutil.rmtree(outdir, ignore_errors=True)
+
+
+def test_pixel_membership_is_the_reference_set_lookup():
+    """loop_idx (analysis.py:117-125: a Python set lookup per disp pixel) by
+    ucl.pixel_membership: binary search on the union's sorted pixel keys, or
+    np.isin for unsorted input -- the reference's booleans either way."""
+    rng = np.random.default_rng(0)
+    for t in range(120):
+        n, nb = int(rng.integers(0, 3000)), int(rng.integers(1, 200))
+        r = rng.integers(0, nb, n)
+        c = r + rng.integers(0, 50, n)
+        k = np.unique(r * 100000 + c)
+        r, c = k // 100000, k % 100000
+        if t % 3 == 0:
+            p = rng.permutation(len(r))
+            r, c = r[p], c[p]
+        cl = [[[[int(i), int(i + d)] for i, d in zip(
+            rng.integers(0, nb + 5, 9), rng.integers(0, 55, 9))]
+            for _ in range(int(rng.integers(0, 4)))] for _ in range(2)]
+        pixels = set().union(*sum([[set(map(tuple, x)) for x in l]
+                                   for l in cl], []))
+        want = np.array([(a, b) in pixels for a, b in zip(r, c)], dtype=bool)
+        got = ucl.pixel_membership(r, c, [[set(map(tuple, x)) for x in l]
+                                          for l in cl])
+        np.testing.assert_array_equal(got, want.reshape(-1))

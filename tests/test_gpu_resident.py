@@ -1,0 +1,114 @@
+"""The product's device-resident prepare_data -> estimate_disp -> lrt path
+(analysis/resident.py) against the host-array path of the same class
+(H3D_RESIDENT=0: numpy scaled / disp_idx, host f, per-chromosome uploads),
+and h3d_scale_disp_dev against the reference's numpy expressions
+(analysis.py:109-115)."""
+import os
+import shutil
+import tempfile
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import e2e_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _numpy_disp_idx(scaled, design, mean_thresh, dist, dist_min):
+    mean = np.dot(scaled, design) / np.sum(design, axis=0)
+    return np.all(mean >= mean_thresh, axis=1) & (dist >= dist_min)
+
+
+@pytest.mark.parametrize('R,C,per_rep', [(4, 2, False), (4, 2, True),
+                                         (9, 3, False), (18, 3, False)])
+def test_scale_disp_matches_numpy(R, C, per_rep):
+    import torch
+    from hic3defdr_amd import _native
+    from hic3defdr_amd.analysis.resident import Resident
+    rng = np.random.default_rng(R * 10 + C)
+    n = 200003
+    bal = rng.gamma(1.2, 2.0, (n, R))
+    bal[rng.random((n, R)) < 0.02] = 0.0
+    bal[rng.random((n, R)) < 0.002] = np.inf      # count / zero bias
+    bal[rng.random((n, R)) < 0.002] = np.nan      # 0 / 0
+    sf = rng.uniform(0.5, 2.0, R if per_rep else (n, R))
+    row = np.sort(rng.integers(0, 20000, n)).astype(np.int32)
+    col = (row + rng.integers(0, 300, n)).astype(np.int32)
+    design = np.zeros((R, C), dtype=bool)
+    design[np.arange(R), np.arange(R) % C] = True
+    mean_thresh = 1.0
+    # rows whose condition means land exactly on the threshold
+    k = rng.choice(n, 5000, replace=False)
+    bal[k] = sf[None, :] if per_rep else sf[k]
+    dist = col - row
+    want_scaled = bal / sf
+    want = _numpy_disp_idx(want_scaled, design, mean_thresh, dist, 4)
+
+    ctx = _native.context(0)
+    dev = torch.device('cuda', ctx.device)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa
+    d_bal, d_sf, d_row, d_col = up(bal), up(sf), up(row), up(col)
+    torch.cuda.synchronize()
+    scaled, flag = ctx.scale_disp_dev(
+        d_bal.data_ptr(), d_sf.data_ptr(), per_rep, d_row.data_ptr(),
+        d_col.data_ptr(), n, R, design, mean_thresh, 4)
+    # scaled bit for bit (IEEE quotients), NaN where numpy has NaN
+    np.testing.assert_array_equal(scaled.view(np.int64),
+                                  want_scaled.view(np.int64))
+    decided = flag != 2
+    np.testing.assert_array_equal(flag[decided] == 1, want[decided])
+    print('R %d C %d: %d of %d rows left to numpy (non-finite or on the '
+          'threshold)' % (R, C, int((~decided).sum()), n))
+    assert (~decided).sum() < 0.1 * n
+
+    # through Resident.scale_disp: every row decided, device flags = host
+    class _H(object):
+        def _ctx(self):
+            return ctx
+    res = Resident(_H())
+    holder = {'bal': d_bal.clone(), 'sf': d_sf, 'row': d_row, 'col': d_col}
+    scaled2, disp_idx = res.scale_disp(holder, design, mean_thresh, 4, dist)
+    np.testing.assert_array_equal(disp_idx, want)
+    np.testing.assert_array_equal(holder['di'].cpu().numpy().astype(bool), want)
+    assert 'bal' not in holder
+
+
+@pytest.mark.parametrize('name', ['small2', 'c3r9'])
+def test_resident_path_equals_host_path(name, monkeypatch):
+    """Every outdir array of run_to_qvalues bit for bit between the resident
+    device path and the host-array path (H3D_RESIDENT=0)."""
+    from hic3defdr_amd import HiC3DeFDR
+    from hic3defdr_amd.analysis import analysis
+    g, kw = e2e_inputs(name)
+    design = pd.DataFrame(kw['design'], index=kw['reps'], columns=kw['conds'])
+    tmp = tempfile.mkdtemp(prefix='h3d_res_')
+    try:
+        hs = {}
+        for mode in (True, False):
+            monkeypatch.setattr(analysis, '_KEEP_RESIDENT', mode)
+            h = HiC3DeFDR(raw_npz_patterns=kw['raw_npz_patterns'],
+                          bias_patterns=kw['bias_patterns'],
+                          chroms=kw['chroms'], design=design,
+                          outdir=os.path.join(tmp, str(mode)),
+                          dist_thresh_max=kw['dist_thresh_max'],
+                          loop_patterns=kw['loop_patterns'], res=10000)
+            h.run_to_qvalues(verbose=False)
+            h.flush()
+            hs[mode] = h
+        names = ['row', 'col', 'raw', 'size_factors', 'scaled', 'disp_idx',
+                 'disp', 'mu_hat_null', 'mu_hat_alt', 'llr', 'pvalues',
+                 'qvalues']
+        if kw['loop_patterns']:
+            names.append('loop_idx')
+        for chrom in kw['chroms']:
+            for s in names:
+                a = hs[True].load_data(s, chrom)
+                b = hs[False].load_data(s, chrom)
+                assert a.dtype == b.dtype, (s, a.dtype, b.dtype)
+                np.testing.assert_array_equal(a, b, err_msg='%s %s' % (s, chrom))
+        np.testing.assert_array_equal(hs[True].load_data('disp_per_dist'),
+                                      hs[False].load_data('disp_per_dist'))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)

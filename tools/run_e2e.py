@@ -75,6 +75,8 @@ def main():
     ap.add_argument('--seed', type=int, default=3)
     ap.add_argument('--keep', default=None,
                     help='write the dataset and outdir here and keep them')
+    ap.add_argument('--profile', type=int, default=0,
+                    help='cProfile the stages, print the top N to stderr')
     args = ap.parse_args()
     import pandas as pd
     from hic3defdr_amd import HiC3DeFDR
@@ -95,7 +97,19 @@ def main():
                       design=design, outdir=os.path.join(base, 'out'),
                       dist_thresh_max=DMAX, loop_patterns=kw['loop_patterns'],
                       res=10000)
+        # process start costs, reported apart: torch's import (the device
+        # allocator; the first _shards() pulls it in) and the HIP context
+        t = time.perf_counter()
+        h._shards()
+        h._ctx()
+        init_s = time.perf_counter() - t
+        print('  init (torch import, HIP context) %.3f s' % init_s,
+              file=sys.stderr, flush=True)
         stages = {}
+        if args.profile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t = time.perf_counter()
         for name, fn in (('prepare_data', lambda: h.prepare_data(verbose=False)),
                          ('estimate_disp', h.estimate_disp),
@@ -109,6 +123,12 @@ def main():
             print('  %s %.3f s' % (name, stages[name + '_s']), file=sys.stderr,
                   flush=True)
         total = sum(stages.values())
+        if args.profile:
+            import pstats
+            prof.disable()
+            for key in ('cumulative', 'tottime'):
+                pstats.Stats(prof, stream=sys.stderr).sort_stats(key) \
+                    .print_stats(args.profile)
         t = time.perf_counter()
         h.collect(fdr=[0.01, 0.05], cluster_size=[3, 4])
         h.flush()
@@ -122,7 +142,7 @@ def main():
             'bins': int(sum(bins)), 'reps': 4, 'conds': 2,
             'dist_thresh_max': DMAX, 'rank': sh.rank, 'world': sh.world,
             'disp_pixels_this_rank': n_disp,
-            'run_to_qvalues_s': total, 'stages': stages,
+            'init_s': init_s, 'run_to_qvalues_s': total, 'stages': stages,
             'pixels_per_s_run_to_qvalues': n_disp / total,
             'estimate_disp_plus_lrt_s': stages['estimate_disp_s'] +
             stages['lrt_s'],
