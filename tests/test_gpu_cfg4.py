@@ -75,8 +75,11 @@ def test_cfg4_full_chromosome(cfg4):
     rel, ddelta = np.array(rel), np.array(ddelta)
     print('cfg4 segments vs the oracle: rel %s, |d delta| %s' % (
         np.array2string(rel, precision=2), np.array2string(ddelta, precision=2)))
-    assert (rel <= 1e-6).sum() >= len(rel) - 1, rel
-    assert np.all(ddelta <= 2e-5), ddelta
+    # measured r04j: every segment within 2.2e-9 of the oracle (|d delta|
+    # <= 1.3e-10); a near-tied Brent comparison flipping would move one by
+    # up to xatol in delta (test_gpu_scale.py)
+    assert np.all(rel <= 1e-6), rel
+    assert np.all(ddelta <= 1e-5), ddelta
 
     # a pixel sample through the oracle's lrt with the GPU's tables
     rng = np.random.default_rng(1)
