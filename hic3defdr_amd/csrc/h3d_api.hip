@@ -159,7 +159,7 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
                       const int64_t* cs, const int32_t* cl, const int32_t* cd,
                       int C, const int32_t* rep_idx, const int32_t* n_rep,
                       const SegState* st, int* seg_flags, const int32_t* list,
-                      const int32_t* meta, double* partial) {
+                      int32_t* meta, double* partial) {
   // equalize pass (heavy: q2qnbinom), then (multi-rank driver) the NLL-only
   // pass (light)
   {
@@ -169,7 +169,7 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
     auto k = k_disp_work<M, WW, kEqualize, NLL>;                                    \
     hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,      \
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep, \
-                       st, seg_flags, list, meta, partial);                         \
+                       st, seg_flags, list, meta, partial, ctx->eq_static8);        \
   } while (0)
     if constexpr (M == 2 && NLL) {
       H3D_EQ(4);
@@ -203,7 +203,7 @@ void launch_disp_work(h3d_ctx* ctx, size_t max_items, const int32_t* raw_s,
     }
     hipLaunchKernelGGL(k, dim3(work_grid(ctx, k, max_items)), dim3(kBlock), 0,
                        ctx->stream, raw_s, f_s, pd, n, cs, cl, cd, C, rep_idx, n_rep,
-                       st, seg_flags, list, meta, partial);
+                       st, seg_flags, list, meta, partial, ctx->eq_static8);
   }
 }
 
@@ -465,6 +465,8 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_NLL_W")) ctx->nll_w = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W8")) ctx->disp_w8 = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W2")) ctx->disp_w2 = std::atoi(e);
+  if (const char* e = std::getenv("H3D_EQ_STATIC8"))
+    ctx->eq_static8 = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
   if (const char* e = std::getenv("H3D_BRENT")) ctx->brent_gang = std::atoi(e);
   if (const char* e = std::getenv("H3D_BRENT_LDS_KB")) ctx->brent_lds_kb = std::atoi(e);
@@ -867,7 +869,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   int64_t* d_lpx = (int64_t*)(d_blob + parts[8].off);
   const size_t max_items = (size_t)std::max(n_chunks, 1) * C;
   int32_t* d_list = (int32_t*)scratch(ctx, "work_list", max_items * 4);
-  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", 16);  // len, active, eq_len, live
+  // len, active, eq_len, live; k_disp_work's task heads (kTaskHeadStride apart)
+  int32_t* d_meta = (int32_t*)scratch(ctx, "work_meta", kWorkMetaInts * 4);
   int32_t* d_slb = (int32_t*)scratch(ctx, "seg_lb", S * 4);
   int32_t* d_sle = (int32_t*)scratch(ctx, "seg_le", S * 4);
   double* d_partial = (double*)scratch(ctx, "partial", max_items * 8 * kWavesPerBlock);

@@ -112,6 +112,9 @@ struct h3d_ctx {
   // Mpx/s; M = 2 at W 4 / 5 / 6: 320 (327) / 317 / 307 -- the gain is
   // k_brent<2> (3.5 vs 3.9 ms), equalize is unchanged (same VGPR profile)
   int disp_w2 = 4;
+  // k_disp_work: eighths of the task rounds dealt statically (the rest from
+  // a device counter); H3D_EQ_STATIC8
+  int eq_static8 = 4;
   int disp_m2 = 1;
   // H3D_BRENT: 1 = gang Brent searches (k_brent_gang) where one workgroup
   // per segment leaves CUs idle, 2 = always, 0 = k_brent only

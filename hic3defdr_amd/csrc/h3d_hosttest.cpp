@@ -82,6 +82,22 @@ int h3dt_equalize(int64_t n, int r, const int32_t* x, const double* f,
   return bad;
 }
 
+// per-pixel NLL terms at delta by the general / mid (r >= 10) / large
+// (r >= 20) forms of the Brent kernels (mode 0 / 1 / 2)
+int h3dt_nll_terms(int64_t n, int r, const double* pseudo, double delta, int mode,
+                   double* out) {
+  if (r < 1 || r > M || mode < 0 || mode > 2) return -1;
+  const h3d::NllConst kc = h3d::nll_const(delta, r);
+  for (int64_t i = 0; i < n; ++i) {
+    double ps[M];
+    for (int k = 0; k < M; ++k) ps[k] = k < r ? pseudo[i * r + k] : 0.0;
+    out[i] = mode == 2   ? h3d::nll_pixel_large<M>(ps, r, kc)
+             : mode == 1 ? h3d::nll_pixel_mid<M>(ps, r, kc)
+                         : h3d::nll_pixel<M>(ps, r, kc);
+  }
+  return 0;
+}
+
 // per-pixel LRT with per-replicate dispersions (lrt.py:7-50)
 int h3dt_lrt(int64_t n, int R, int C, const int32_t* raw, const double* f,
              const double* disp_wide, const int32_t* cond_of_rep, int refit,

@@ -356,6 +356,11 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
 // NLL = false (single-rank driver): the equalize pass only writes the
 // pseudodata; k_brent then evaluates every NLL of the segment's Brent search
 // in one workgroup.
+// k_disp_work's dynamic task heads in the work meta: 2 passes x 8 ranges,
+// kTaskHeadStride ints (128 B) apart, after the first block of the meta
+constexpr int kTaskHeadStride = 32;
+constexpr int kWorkMetaInts = kTaskHeadStride * 17;
+
 template <int M, int W, int PH, bool NLL = true>
 __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     const int32_t* __restrict__ raw_s, const double* __restrict__ f_s,
@@ -364,18 +369,56 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     int C, const int32_t* __restrict__ rep_idx /* C x kMaxReps */,
     const int32_t* __restrict__ n_rep /* C */, const SegState* __restrict__ st,
     int* __restrict__ seg_flags, const int32_t* __restrict__ list,
-    const int32_t* __restrict__ meta /* [len, active, eq_len] */,
-    double* __restrict__ partial) {
+    int32_t* __restrict__ meta /* [len, active, eq_len, live], task heads */,
+    double* __restrict__ partial, int static8) {
   const int beg = (PH == kEqualize) ? 0 : meta[2];
   const int end = (PH == kEqualize) ? meta[2] : meta[0];
-  for (int w = beg + blockIdx.x; w < end; w += gridDim.x) {
+  // Tasks are (item, wave) pairs: wave q of a block evaluates pixels
+  // [64 q, 64 q + 64) of an item, and the waves run independently (no block
+  // barrier). The first static8 / 8 of the rounds are dealt round-robin; the
+  // remaining tasks are split into 8 ranges, each with its own head counter
+  // (128 B apart, zeroed by k_seg_update): a wave dequeues from the range of
+  // its block group (blockIdx % 8 -- the blocks of one XCD under the
+  // observed round-robin placement; speed only), then from the others once
+  // that range is spent. The item costs vary with the incomplete-gamma trip
+  // counts, and a static deal left the waves that drew the dearer items
+  // running alone at the end of the launch; one head for every wave
+  // saturates (~88 dequeues / us, MI355X_MICROARCH.md "dequeue").
+  constexpr int kWv = kBlock / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t t0 = (int64_t)beg * kWv, t1 = (int64_t)end * kWv;
+  const int64_t wt = (int64_t)gridDim.x * kWv;
+  const int64_t tdyn = t0 + ((t1 - t0) / wt) * static8 / 8 * wt;
+  const int64_t tl = t1 - tdyn;
+  int32_t* heads = meta + kTaskHeadStride * (1 + (PH == kEqualize ? 0 : 8));
+  const int grp = blockIdx.x & 7;
+  unsigned spent = 0u;
+  auto take = [&]() -> int64_t {
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+      const int p = (grp + k) & 7;
+      if ((spent >> p) & 1u) continue;
+      const int64_t pb = tdyn + tl * p / 8, pe = tdyn + tl * (p + 1) / 8;
+      int got = 0;
+      if (lane == 0) got = atomicAdd(heads + kTaskHeadStride * p, 1);
+      got = __shfl(got, 0, 64);
+      if (pb + got < pe) return pb + got;
+      spent |= 1u << p;
+    }
+    return t1;
+  };
+  int64_t t = t0 + (int64_t)blockIdx.x * kWv + (threadIdx.x >> 6);
+  if (t >= tdyn) t = take();
+  for (; t < t1; t = (t + wt < tdyn) ? t + wt : take()) {
+    const int w = (int)(t / kWv);
+    const int q = (int)(t - (int64_t)w * kWv);
     const int item = list[w];
     const int chunk = item / C, c = item - chunk * C;
     const int s = chunk_d[chunk] * C + c;
     constexpr int phase = PH;
     const int nr = n_rep[c];
     double term = 0.0;
-    const int i = threadIdx.x;
+    const int i = q * 64 + lane;
     if (i < chunk_len[chunk] && nr < 8) {
       // Rolled replicate loop: the q2qnbinom code (the bulk of the kernel)
       // is emitted once instead of once per replicate slot. Sums run
@@ -495,8 +538,8 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     // one partial per wave (fixed shuffle tree -> deterministic); no block
     // barrier, so the waves of a block run their items independently
     if constexpr (NLL) {
-      const double t = wave_sum(term);
-      if ((threadIdx.x & 63) == 0) partial[(int64_t)w * kWavesPerBlock + (threadIdx.x >> 6)] = t;
+      const double wt_sum = wave_sum(term);
+      if (lane == 0) partial[(int64_t)w * kWavesPerBlock + q] = wt_sum;
     }
   }
 }
@@ -685,6 +728,8 @@ static __global__ __launch_bounds__(1024) void k_seg_update(
     // the host loop terminates on
     meta[3] = live_total;
   }
+  // k_disp_work's dynamic task heads (2 passes x 8 ranges)
+  if (threadIdx.x < 16) meta[kTaskHeadStride * (1 + threadIdx.x)] = 0;
 }
 
 // The whole bounded-Brent search of cml (dispersion.py:46-80) for every
@@ -713,9 +758,10 @@ static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int 
 // scheduler interleaves (the NLL is bound by FP64 dependency latency at 4
 // waves/SIMD); the terms still join the sum in pixel order (M >= 8: one
 // pixel per trip -- the pair spilled at the 128-VGPR budget of
-// __launch_bounds__(512, 4)). LARGE: every argument >= kNllLargeR
+// __launch_bounds__(512, 4)). MODE 2: every argument >= kNllLargeR
+// (nll_pixel_large); 1: >= kNllMidR (nll_pixel_mid); 0: nll_pixel.
 // (nll_pixel_large).
-template <int M, int kBlockT, bool LARGE>
+template <int M, int kBlockT, int MODE>
 __device__ __forceinline__ double brent_segment_sum(
     const double* s_pd, int64_t lds_px, const double* __restrict__ pd, int64_t n,
     const int* ri, int nr, int64_t b, int64_t el, int64_t e, const NllConst& kc,
@@ -723,7 +769,9 @@ __device__ __forceinline__ double brent_segment_sum(
   double acc = 0.0;
   constexpr int kPair = M <= 4 ? 2 : 1;
   auto term = [&](const double* v) {
-    return LARGE ? nll_pixel_large<M>(v, nr, kc, s_tab) : nll_pixel<M>(v, nr, kc, s_tab);
+    if constexpr (MODE == 2) return nll_pixel_large<M>(v, nr, kc, s_tab);
+    else if constexpr (MODE == 1) return nll_pixel_mid<M>(v, nr, kc, s_tab);
+    else return nll_pixel<M>(v, nr, kc, s_tab);
   };
   for (int64_t i = threadIdx.x; i < el - b; i += kPair * kBlockT) {
     const int64_t j = i + kBlockT;
@@ -820,11 +868,14 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     __syncthreads();
     while (true) {
       const NllConst kc = s_st.k;
-      // every lgamma argument >= r: at r >= kNllLargeR the short path
-      // (nll_pixel_large), the same for every thread of the segment
+      // every lgamma argument >= r: at r >= kNllLargeR / kNllMidR the short
+      // paths (nll_pixel_large / _mid), the same for every thread of the
+      // segment
       const double acc = (kc.r >= kNllLargeR)
-          ? brent_segment_sum<M, kBrentBlock, true>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
-          : brent_segment_sum<M, kBrentBlock, false>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab);
+          ? brent_segment_sum<M, kBrentBlock, 2>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
+          : (kc.r >= kNllMidR)
+          ? brent_segment_sum<M, kBrentBlock, 1>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
+          : brent_segment_sum<M, kBrentBlock, 0>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab);
       double wacc = acc;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) wacc += __shfl_xor(wacc, off, 64);
@@ -842,6 +893,7 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
       if (!s_more) break;
     }
     if (threadIdx.x == 0) {
+      s_st.last_evals = evals;
       st[s] = s_st;
       if (s_st.phase == kDone) result[s] = s_st.result;
       atomicAdd(&work_count[1], (unsigned long long)(e - b) * nr * evals);
@@ -956,8 +1008,10 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
       const NllConst kc = s_st.k;
       // the slice (no LDS head), two pixels per trip for M <= 4, as k_brent
       double acc = (kc.r >= kNllLargeR)
-          ? brent_segment_sum<M, kGangThreads, true>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab)
-          : brent_segment_sum<M, kGangThreads, false>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab);
+          ? brent_segment_sum<M, kGangThreads, 2>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab)
+          : (kc.r >= kNllMidR)
+          ? brent_segment_sum<M, kGangThreads, 1>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab)
+          : brent_segment_sum<M, kGangThreads, 0>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) wpart[wid] = acc;

@@ -8,11 +8,7 @@
 // (M / 8 slots), so the row reads are 8 contiguous values per group and the
 // per-lane state is M / 8 slots.
 //
-// Sums over replicates go through a 3-level xor butterfly inside the group.
-// For the two log-likelihood rows that butterfly IS numpy's association
-// (pairwise_sum, n >= 8: accumulator j sums elements j, j + 8, ... of the
-// 8-aligned block, then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)),
-// then the n % 8 tail in order) -- the same bits as lrt_pixel's np_sum, and
+// Sums over replicates go through a 3-level xor butterfly inside the group:
 // every lane of the group ends with the same value (IEEE addition commutes),
 // so the Newton iterations of the group stay in lockstep and the group exits
 // its loops together.
@@ -37,34 +33,14 @@ __device__ inline int gor8(int v) {
   return v;
 }
 
-// numpy's sum of a group-distributed row of n >= 8 values (element k in lane
-// k % 8, slot k / 8): the slot loop per lane, the butterfly, the tail.
-template <int J>
-__device__ inline double np_sum_g8(const double* v, int n, int lane, int base) {
-  const int blk = n - n % 8;
-  double r = v[0];
-#pragma unroll
-  for (int s = 1; s < J; ++s)
-    if (lane + 8 * s < blk) r += v[s];
-  double res = gsum8(r);
-  // tail: elements blk .. n-1 all sit in slot blk / 8
-  const int st = blk / 8;
-  double tv = 0.0;
-#pragma unroll
-  for (int s = 0; s < J; ++s)
-    if (s == st) tv = v[s];
-  for (int t = 0; t < n - blk; ++t) res += __shfl(tv, base + t, 64);
-  return res;
-}
-
-// fit_mu (h3d_model.h) over the group: same bracketed Newton on
-// g(theta) = mu S(mu), sums by butterfly (any fixed order; the root is
-// unique and the solve runs to full precision). `slots` = this lane's bits of
+// fit_mu (h3d_model.h) over the group: the same bracketed Halley steps on
+// g(theta) = mu S(mu) from sum(x) / sum(b), sums by butterfly (any fixed
+// order; the root is unique and the solve runs to full precision). `slots` = this lane's bits of
 // the fit's replicate mask (bit s: replicate lane + 8 s).
 template <int J>
 __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
                             unsigned slots, int* status) {
-  double sx = 0.0, init = 0.0, cnt = 0.0;
+  double sx = 0.0, sb = 0.0;
   int bad = 0;
 #pragma unroll
   for (int s = 0; s < J; ++s)
@@ -74,13 +50,11 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
                  ? 1
                  : 0;
       sx += (double)x[s];
-      init += (double)x[s] / b[s];
-      cnt += 1.0;
+      sb += b[s];
     }
   bad = gor8(bad);
   sx = gsum8(sx);
-  init = gsum8(init);
-  cnt = gsum8(cnt);
+  sb = gsum8(sb);
   if (bad) {
     *status |= kFlagBadInput;
     return NAN;
@@ -89,29 +63,35 @@ __device__ double fit_mu_g8(const int32_t* x, const double* b, const double* a,
     *status |= kFlagNoRoot;
     return NAN;
   }
-  double th = log_fast_checked(init / cnt);
+  double th = log_fast_checked(div_fast(sx, sb));
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
     const double mu = exp_fast(th);
-    double g = 0.0, gp = 0.0;
+    double g = 0.0, gp = 0.0, gpp = 0.0;
 #pragma unroll
     for (int s = 0; s < J; ++s)
       if ((slots >> s) & 1u) {
         const double mb = mu * b[s];
-        const double den = 1.0 / (1.0 + a[s] * mb);
+        const double am = a[s] * mb;
+        const double den = recip_fast(1.0 + am);
         g += ((double)x[s] - mb) * den;
-        gp -= mb * (1.0 + a[s] * (double)x[s]) * den * den;
+        const double t = mb * (1.0 + a[s] * (double)x[s]) * den * den;
+        gp -= t;
+        gpp -= t * (1.0 - 2.0 * am * den);
       }
     g = gsum8(g);
     gp = gsum8(gp);
+    gpp = gsum8(gpp);
     if (g > 0.0)
       lo = th;
     else if (g < 0.0)
       hi = th;
     else
       return mu;
-    const double dn = g / gp;
-    if (fabs(dn) <= 1e-8 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
+    const double nt = g * recip_fast(gp);
+    const double hf = 1.0 - 0.5 * nt * gpp * recip_fast(gp);
+    const double dn = (hf >= 0.5 && hf <= 2.0) ? nt * recip_fast(hf) : nt;
+    if (fabs(dn) <= 1e-5 * fmax(1.0, fabs(th))) return exp_fast(th - dn);
     double tn = th - dn;
     if (!(tn > lo && tn < hi)) {
       if (is_inf(lo))
@@ -226,25 +206,31 @@ __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
       for (int c = 0; c < CM; ++c)
         if (c == t - 1) m1[c] = mu;
     }
-    // log-likelihood rows (lrt_pixel: same terms, same bits per replicate)
-    double tn[J], ta[J];
+    // llr as lrt_pixel forms it: per replicate x log(mu0 / mu1) - (r + x)
+    // log((r + m0) / (r + m1)) (the logpmf rows' difference term by term),
+    // one log per replicate and one per condition
+    double lq[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      lq[c] = (c < C) ? log_fast_checked(div_fast(m0, m1[c]), s_tab) : 0.0;
+    double part = 0.0;
 #pragma unroll
     for (int s = 0; s < J; ++s) {
-      double m1k = 0.0;
+      if (lane + kGroup * s >= R) continue;
+      double m1k = 0.0, l = 0.0;
 #pragma unroll
       for (int c = 0; c < CM; ++c)
-        if (c == cnd[s]) m1k = m1[c];
+        if (c == cnd[s]) {
+          m1k = m1[c];
+          l = lq[c];
+        }
       const double xk = (double)x[s];
       const double r = 1.0 / a[s];
-      // the mean-free prefix of logpmf is common to the null and alt rows
-      // and cancels in llr: left out, as k_lrt (lrt_pixel)
-      const double m0k = m0 * fv[s], m1f = m1k * fv[s];
-      const double l0 = log_fast_checked(r + m0k, s_tab);
-      const double l1 = log_fast_checked(r + m1f, s_tab);
-      tn[s] = -r * l0 + xk * log_fast_checked(m0k, s_tab) - xk * l0;
-      ta[s] = -r * l1 + xk * log_fast_checked(m1f, s_tab) - xk * l1;
+      const double lr =
+          log_fast_checked(div_fast(r + m0 * fv[s], r + m1k * fv[s]), s_tab);
+      part += xk * l - (r + xk) * lr;
     }
-    const double lv = np_sum_g8<J>(tn, R, lane, base) - np_sum_g8<J>(ta, R, lane, base);
+    const double lv = gsum8(part);
     fl_all |= st;
     if (lane == 0) {
       p[i] = chi2_sf((double)(C - 1), -2 * lv);

@@ -415,33 +415,38 @@ H3D_HD int lrt_pixel(const TX* x, const double* f, const double* a,
     for (int c = 0; c < CM; ++c)
       if (c == t - 1) mu1[c] = mu;
   }
-  // the two log-likelihood rows are summed as they are produced
-  // (NpSumStream: numpy's association without the two M-long rows)
-  NpSumStream tn(R), ta(R);
+  // llr = sum(null logpmf row) - sum(alt logpmf row) (lrt.py:42-48) per
+  // replicate k, with m0 = mu0 f_k, m1 = mu1[c(k)] f_k, r = 1 / disp_k
+  // (scaled_nb.py:31-33):
+  //   gammaln(r + x) - gammaln(x + 1) - gammaln(r) + r log r  cancels,
+  //   x log m0 - x log m1 = x log(mu0 / mu1)                (f_k cancels),
+  //   -(r + x) log(r + m0) + (r + x) log(r + m1) = -(r + x) log((r + m0) / (r + m1)),
+  // so one log per replicate and one per condition instead of four per
+  // replicate -- and without the cancellation of two O(1e3) row sums that
+  // leaves the reference's llr ~1e-13 of noise (the rows' rounding; the
+  // p-values move by that only).
+  double lq[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    lq[c] = (c < C) ? log_fast_checked(div_fast(*mu0, mu1[c]), tab) : 0.0;
+  double acc = 0.0;
 #pragma unroll
   for (int k = 0; k < M; ++k) {
     if (k < R) {
-      double m1 = 0.0;
+      double m1 = 0.0, l = 0.0;
 #pragma unroll
       for (int c = 0; c < CM; ++c)
-        if (c == cond[k]) m1 = mu1[c];
-      // logpmf (scaled_nb.py:31-33) under the null and the alt mean. The
-      // terms without m -- gammaln(r + k) - gammaln(k + 1) - gammaln(r) +
-      // r log r, Python's left-to-right prefix -- are the same in the null
-      // and the alt row of a replicate and cancel in llr = sum(null) -
-      // sum(alt) exactly; only the rows' rounding sees them (the reference's
-      // rows carry ~ulp(gammaln(r + k)) of it). They are left out: llr moves
-      // by that rounding only (12 lgammas + 4 logs per pixel fewer)
+        if (c == cond[k]) {
+          m1 = mu1[c];
+          l = lq[c];
+        }
       const double xk = (double)x[k];
       const double r = 1.0 / a[k];
-      const double m0k = *mu0 * f[k], m1k = m1 * f[k];
-      const double l0 = log_fast_checked(r + m0k, tab);
-      const double l1 = log_fast_checked(r + m1k, tab);
-      tn.add(k, -r * l0 + xk * log_fast_checked(m0k, tab) - xk * l0);
-      ta.add(k, -r * l1 + xk * log_fast_checked(m1k, tab) - xk * l1);
+      const double lr = log_fast_checked(div_fast(r + *mu0 * f[k], r + m1 * f[k]), tab);
+      acc += xk * l - (r + xk) * lr;
     }
   }
-  *llr = tn.sum() - ta.sum();
+  *llr = acc;
   *p = chi2_sf((double)(C - 1), -2 * *llr);
   return st;
 }
@@ -490,6 +495,22 @@ H3D_HD double nll_pixel_large(const double* d, int n, const NllConst& k,
 
 constexpr double kNllLargeR = 20.0;
 
+// nll_pixel where every lgamma argument is >= 10 (r >= 10): nll_pixel's
+// terms without its shift products (all 1 there, so its ln of their product
+// is 0) -- the Brent kernels take it for 10 <= r < kNllLargeR, the usual
+// optimum region of the searches
+template <int M>
+H3D_HD double nll_pixel_mid(const double* d, int n, const NllConst& k,
+                            const LogTab* tab = kLogTab) {
+  double lg[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) lg[j] = (j < n) ? lgam_nll_mid(d[j] + k.r, tab) : 0.0;
+  const double z = np_sum<M>(d, n);
+  const double lz = lgam_nll_mid(z + k.nr, tab);
+  return np_sum<M>(lg, n) + k.lg_nr - lz - k.n_lg_r;
+}
+constexpr double kNllMidR = 10.0;
+
 template <int M>
 H3D_HD double nll_pixel(const double* d, int n, const NllConst& k,
                         const LogTab* tab = kLogTab) {
@@ -536,7 +557,7 @@ struct SegState {
   int num;
   int qiter;
   int evals;  // NLL evaluations over every Brent search of the segment
-  int pad_;
+  int last_evals;  // ... of its latest search (k_brent's queue order)
   double disp;    // current qcml dispersion (used by the equalize pass)
   double x;       // delta at which the next NLL is evaluated
   double result;  // final qcml dispersion (NaN for an empty segment)
@@ -555,7 +576,7 @@ H3D_HD void seg_init(SegState* s, long long n_px, int n_reps) {
   s->num = 0;
   s->qiter = 0;
   s->evals = 0;
-  s->pad_ = 0;
+  s->last_evals = 0;
   s->disp = 0.01;
   s->x = brent_x0();
   s->k = nll_const(s->x, n_reps);

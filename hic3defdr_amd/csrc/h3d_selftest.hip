@@ -132,6 +132,19 @@ __global__ void k_equalize_nll(int64_t n, int r, const int32_t* __restrict__ x,
   if (st_all) atomicOr(status, st_all);
 }
 
+__global__ void k_nll_terms(int64_t n, int r, const double* __restrict__ pseudo,
+                            h3d::NllConst kc, int mode, double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double ps[M];
+#pragma unroll
+    for (int k = 0; k < M; ++k) ps[k] = (k < r) ? pseudo[i * r + k] : 0.0;
+    out[i] = mode == 2   ? h3d::nll_pixel_large<M>(ps, r, kc)
+             : mode == 1 ? h3d::nll_pixel_mid<M>(ps, r, kc)
+                         : h3d::nll_pixel<M>(ps, r, kc);
+  }
+}
+
 __global__ void k_lrt(int64_t n, int R, int C, const int32_t* __restrict__ raw,
                       const double* __restrict__ f,
                       const double* __restrict__ disp_wide,
@@ -297,6 +310,18 @@ int h3dt_equalize(int64_t n, int r, const int32_t* x, const double* f,
   dp.to_host(out);
   dst.to_host(&st);
   return g_failed ? -2 : st;
+}
+
+int h3dt_nll_terms(int64_t n, int r, const double* pseudo, double delta, int mode,
+                   double* out) {
+  if (r < 1 || r > M || mode < 0 || mode > 2) return -1;
+  Dev<double> dp(pseudo, n * r), dout_(nullptr, n);
+  const h3d::NllConst kc = h3d::nll_const(delta, r);
+  hipLaunchKernelGGL(k_nll_terms, dim3(grid_of(n)), dim3(kBlock), 0, 0, n, r, dp.p, kc, mode,
+                     dout_.p);
+  if (!sync_ok()) return -2;
+  dout_.to_host(out);
+  return g_failed ? -2 : 0;
 }
 
 int h3dt_lrt(int64_t n, int R, int C, const int32_t* raw, const double* f,

@@ -480,6 +480,18 @@ H3D_HD double lgam_nll_large(double x, const LogTab* tab = kLogTab) {
   return (x - 0.5) * log_fast(x, tab) - x + kLogSqrt2Pi + corr;
 }
 
+// lgam_nll_parts for x >= 10 (the caller knows it for every lane: the NLL
+// arguments d + r with r >= 10): no shift product, the 8-term series -- the
+// same terms lgam_nll_parts evaluates there, without the product's bookkeeping
+H3D_HD double lgam_nll_mid(double x, const LogTab* tab = kLogTab) {
+#if defined(__clang__)
+#pragma clang fp contract(fast)
+#endif
+  const double r = recip_nll(x), r2 = r * r;
+  const double corr = r * stirling_nll(r2);
+  return (x - 0.5) * log_fast(x, tab) - x + kLogSqrt2Pi + corr;
+}
+
 // lgam_nll split for batching: returns lgam(x) + ln P and sets *P, the
 // shift product (1 for x >= 10), so a caller summing several lgammas takes
 // ONE log of the combined product (nll_pixel: per pixel R_c + 1 lgammas, one

@@ -30,6 +30,13 @@ I = ctypes.POINTER(ctypes.c_int32)
 def lib(request):
     if request.param == 'host':
         return ctypes.CDLL(h3dbuild.build_hosttest())
+    # one HIP runtime per process: torch's first, as _native.load_library
+    # does (the selftest library loaded first leaves torch without devices
+    # for the GPU tests that run after this module)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     # prebuilt in-tree by build() (the GPU box does not compile)
     path = os.path.join(h3dbuild.LIBDIR, 'libh3d_selftest.so')
     if not os.path.exists(path):
@@ -157,6 +164,36 @@ def test_fit_mu_is_converged_to_full_precision(lib):
     lo, hi = score(mu * (1 - 1e-12)), score(mu * (1 + 1e-12))
     # S decreases through the root: S(mu (1 - eps)) >= 0 >= S(mu (1 + eps))
     assert np.all(lo >= 0) and np.all(hi <= 0)
+
+
+def test_nll_term_forms_agree(lib):
+    """The Brent kernels' NLL term (dispersion.py:67-70) by its general form
+    and by the mid (r >= 10: no shift products) and large (r >= 20: 5-term
+    Stirling) forms: within 1e-14 of the term's largest lgamma of each other
+    and of scipy's gammaln (the term is a difference of lgammas)."""
+    from scipy.special import gammaln
+    rng = np.random.default_rng(11)
+    for r in (2, 4):
+        pd = np.ascontiguousarray(np.concatenate([
+            rng.gamma(0.7, 3.0, (4000, r)), rng.gamma(2.0, 60.0, (4000, r)),
+            np.zeros((50, r))]))
+        n = len(pd)
+        for delta, modes in ((0.09, (0, 1)), (0.0476, (0, 1, 2)),
+                             (0.01, (0, 1, 2)), (0.3, (0,))):
+            rr = 1.0 / delta - 1.0
+            want = (gammaln(pd + rr).sum(1) + gammaln(r * rr)
+                    - gammaln(pd.sum(1) + r * rr) - r * gammaln(rr))
+            got = {}
+            for m in modes:
+                out = np.empty(n)
+                assert lib.h3dt_nll_terms(ctypes.c_int64(n), r, _p(pd),
+                                          ctypes.c_double(delta), m, _p(out)) == 0
+                got[m] = out
+                scale = np.maximum(1.0, gammaln(pd.sum(1) + r * rr))
+                err = np.max(np.abs(out - want) / scale)
+                assert err < 1e-14, (r, delta, m, err)
+            for m in modes[1:]:
+                assert np.max(np.abs(got[m] - got[0]) / scale) < 1e-14
 
 
 def test_fit_mu_doctest_brentq_case(lib):
