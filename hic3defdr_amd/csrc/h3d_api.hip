@@ -708,59 +708,6 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         hipLaunchKernelGGL(k_gather_cond_tile, dim3(grid), dim3(256), 0, s, idx_out, d_raw,
                            d_f, n, R, reps_c, nrep[c], rows);
       }
-    } else if (ctx->disp_sort == 3 && end_bit <= 16) {
-      // the same order as disp_sort 2 -- per condition (distance, min code,
-      // max code), stable -- built as a distance-stable sort (one radix pass
-      // at D <= 256) and ONE random row gather of every replicate into
-      // distance-sorted SoA rows, then per condition a segmented sort of the
-      // 16-bit count codes inside each distance and a gather that stays
-      // inside the segment (its rows L2-resident); disp_sort 2 sorts the
-      // whole array per condition and gathers each condition's rows from the
-      // AoS array at random
-      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, d_dist, dist_s,
-                                                 idx_in, idx_out, (int)n, 0, end_bit, s));
-      void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
-      if (!tmp) return fail(H3D_ENOMEM, "sort temp");
-      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
-                                                 idx_out, (int)n, 0, end_bit, s));
-      int32_t* raw_d = (int32_t*)scratch(ctx, "raw_d", (size_t)n * R * 4);
-      double* f_d = (double*)scratch(ctx, "f_d", (size_t)n * R * 8);
-      uint16_t* codes = (uint16_t*)scratch(ctx, "codes", (size_t)n * 2);
-      uint16_t* codes_s = (uint16_t*)scratch(ctx, "codes_s", (size_t)n * 2);
-      int32_t* perm_c = (int32_t*)scratch(ctx, "idx_out_c", (size_t)n * 4);
-      if (!raw_d || !f_d || !codes || !codes_s || !perm_c)
-        return fail(H3D_ENOMEM, "sort buffers");
-      SoaRows all;
-      for (int r = 0; r < R; ++r) {
-        all.raw[r] = raw_d + (size_t)r * n;
-        all.f[r] = f_d + (size_t)r * n;
-      }
-      hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                         idx_out, d_raw, d_f, n, R, all);
-      hipLaunchKernelGGL(k_seg_bounds, dim3((D + 1 + 255) / 256), dim3(256), 0, s,
-                         dist_s, n, D, d_seg);
-      for (int c = 0; c < C; ++c) {
-        SoaRows src, dst;
-        for (int j = 0; j < nrep[c]; ++j) {
-          const int r = rep_idx[(size_t)c * kMaxReps + j];
-          src.raw[j] = all.raw[r];
-          src.f[j] = all.f[r];
-          dst.raw[j] = raw_s + (size_t)r * n;
-          dst.f[j] = f_s + (size_t)r * n;
-        }
-        hipLaunchKernelGGL(k_cond_codes, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, src,
-                           nrep[c], n, codes, idx_in);
-        size_t sb = 0;
-        HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            nullptr, sb, codes, codes_s, idx_in, perm_c, (int)n, D, d_seg, d_seg + 1, 0, 16,
-            s));
-        void* stmp = scratch(ctx, "cub_tmp_seg", sb);
-        if (!stmp) return fail(H3D_ENOMEM, "segmented sort temp");
-        HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            stmp, sb, codes, codes_s, idx_in, perm_c, (int)n, D, d_seg, d_seg + 1, 0, 16, s));
-        hipLaunchKernelGGL(k_gather_cond_local, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
-                           perm_c, n, nrep[c], src, dst);
-      }
     } else if (ctx->disp_sort == 1 && end_bit <= 16) {
       // (distance, total count) keys: same segments, less lane divergence;
       // 32-bit keys (16 count bits) whenever the distance fits 16 bits
@@ -803,7 +750,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, d_dist, dist_s, idx_in,
                                                  idx_out, (int)n, 0, end_bit, s));
     }
-    if (ctx->disp_sort != 2 && !(ctx->disp_sort == 3 && end_bit <= 16)) {
+    if (ctx->disp_sort != 2) {
       SoaRows rows;
       for (int r = 0; r < R; ++r) {
         rows.raw[r] = raw_s + (size_t)r * n;

@@ -209,40 +209,6 @@ __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
   }
 }
 
-// disp_sort 3: a condition's 16-bit count code (min code << 8 | max code,
-// the low bits of k_dist_cond_keys' key) from the distance-sorted SoA rows
-// (coalesced), and the identity permutation the segmented sort carries
-static __global__ void k_cond_codes(SoaRows rows, int nr, int64_t n,
-                                    uint16_t* __restrict__ codes,
-                                    int32_t* __restrict__ iota) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t mx = 0, mn = ~0ull;
-    for (int j = 0; j < nr; ++j) {
-      const uint64_t v = (uint32_t)rows.raw[j][i];
-      mx = v > mx ? v : mx;
-      mn = v < mn ? v : mn;
-    }
-    codes[i] = (uint16_t)((count_code8(mn) << 8) | count_code8(mx));
-    iota[i] = (int32_t)i;
-  }
-}
-
-// disp_sort 3: a condition's rows through its in-segment order (perm holds
-// distance-sorted positions of the same segment, so the reads stay within
-// one segment's rows -- L2-resident -- instead of the whole array)
-static __global__ void k_gather_cond_local(const int32_t* __restrict__ perm, int64_t n,
-                                           int nr, SoaRows src, SoaRows dst) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = perm[i];
-    for (int k = 0; k < nr; ++k) {
-      dst.raw[k][i] = src.raw[k][j];
-      dst.f[k][i] = src.f[k][j];
-    }
-  }
-}
-
 // sort key (distance, total count capped to cbits bits): inside a distance
 // segment pixels of similar depth sit in the same wave, so the q2qnbinom
 // branches (tail side, series vs continued fraction) diverge less. The count

@@ -264,32 +264,3 @@ def test_union_whole_matrix_keeps_only_the_band(ctx):
     assert np.any(np.isinf(bal)) and np.any(bias[row] * bias[col] == 0)
     assert np.all((col - row >= 0) & (col - row <= dmax))
 
-
-def test_disp_sort_modes_give_the_same_order(monkeypatch):
-    """H3D_DISP_SORT 3 (a distance-stable sort, one random gather of every
-    replicate, then per condition a segmented sort of the count codes and a
-    gather inside each segment) builds the same per-condition pixel order as
-    mode 2 (a stable sort of (distance, min code, max code) keys per
-    condition): estimate_disp bit for bit on a cfg2-shaped band."""
-    import torch
-    from hic3defdr_amd import _native, synthetic
-    raw, f, dist = synthetic.draw_band(4000, (2, 2), 250, seed=3,
-                                       chrom_index=0)
-    cond = np.array([0, 0, 1, 1])
-    dev = torch.device('cuda', 0)
-    t_raw = torch.from_numpy(np.ascontiguousarray(raw, dtype=np.int32)).to(dev)
-    t_f = torch.from_numpy(np.ascontiguousarray(f)).to(dev)
-    t_d = torch.from_numpy(np.ascontiguousarray(dist, dtype=np.int32)).to(dev)
-    torch.cuda.synchronize()
-    out = {}
-    for mode in ('2', '3'):
-        monkeypatch.setenv('H3D_DISP_SORT', mode)
-        c = _native.Context(0)
-        try:
-            out[mode] = c.disp_per_dist_dev(t_raw.data_ptr(), t_f.data_ptr(),
-                                            t_d.data_ptr(), len(raw), 4, cond,
-                                            2, 251)
-        finally:
-            c.close()
-    assert np.isfinite(out['2'][4:]).all()
-    np.testing.assert_array_equal(out['2'], out['3'])
