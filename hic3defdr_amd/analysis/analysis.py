@@ -96,25 +96,46 @@ class AnalyzingHiC3DeFDR(object):
         """Reference ``analysis.py:28-133``."""
         if n_bins == -1:
             n_bins = int(self.dist_thresh_max / 5)
-        if chrom is None:
-            sh = self._shards()
-            for c in sh.mine:
-                self.prepare_data(chrom=c, norm=norm, n_bins=n_bins,
-                                  verbose=verbose)
-            sh.barrier()
-            return
         if norm not in NATIVE_NORMS:
             raise NotImplementedError(
                 'norm=%r: the GPU path implements %s' % (norm, NATIVE_NORMS))
-        eprint('preparing data for chrom %s' % chrom, skip=not verbose)
-        bias = self.load_bias(chrom)
-        # the replicates' NPZ files decompress concurrently (zlib inflate and
-        # crc32 release the GIL)
+        if chrom is None:
+            sh = self._shards()
+            # the next chromosome's files (NPZ inflate, bias, clusters) are
+            # read on threads while this one is prepared
+            with concurrent.futures.ThreadPoolExecutor(1) as pre:
+                nxt = pre.submit(self._prepare_inputs, sh.mine[0]) \
+                    if sh.mine else None
+                for i, c in enumerate(sh.mine):
+                    inputs = nxt.result()
+                    nxt = pre.submit(self._prepare_inputs, sh.mine[i + 1]) \
+                        if i + 1 < len(sh.mine) else None
+                    self._prepare_chrom(c, norm, n_bins, verbose, inputs)
+            sh.barrier()
+            return
+        self._prepare_chrom(chrom, norm, n_bins, verbose,
+                            self._prepare_inputs(chrom))
+
+    def _prepare_inputs(self, chrom):
+        """One chromosome's input files: bias (load_bias), the replicates'
+        canonical CSR matrices (their NPZ archives inflated concurrently:
+        zlib inflate and crc32 release the GIL) and the loop clusters."""
         with concurrent.futures.ThreadPoolExecutor(
                 min(8, len(self.raw_npz_patterns))) as ex:
-            mats = list(ex.map(_canonical_csr,
-                               [p.replace('<chrom>', chrom)
-                                for p in self.raw_npz_patterns]))
+            fut = [ex.submit(_canonical_csr, p.replace('<chrom>', chrom))
+                   for p in self.raw_npz_patterns]
+            bias = self.load_bias(chrom)
+            cl = [load_clusters(p.replace('<chrom>', chrom))
+                  for p in self.loop_patterns.values()] \
+                if self.loop_patterns else None
+            mats = [f.result() for f in fut]
+        return bias, mats, cl
+
+    def _prepare_chrom(self, chrom, norm, n_bins, verbose, inputs):
+        """prepare_data of one chromosome (analysis.py:28-133) from its
+        input files (_prepare_inputs)."""
+        eprint('preparing data for chrom %s' % chrom, skip=not verbose)
+        bias, mats, cl = inputs
         ctx = self._ctx()
         res = self._resident() if _KEEP_RESIDENT else None
         holder = {}
@@ -149,8 +170,6 @@ class AnalyzingHiC3DeFDR(object):
                 (dist >= self.dist_thresh_min)
         if self.loop_patterns:
             eprint('  making loop_idx', skip=not verbose)
-            cl = [load_clusters(p.replace('<chrom>', chrom))
-                  for p in self.loop_patterns.values()]
             loop_idx = pixel_membership(row[disp_idx], col[disp_idx], cl)
             self.save_data(loop_idx, 'loop_idx', chrom)
         eprint('  saving data to disk', skip=not verbose)
