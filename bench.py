@@ -615,6 +615,89 @@ def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
     }
 
 
+OTHER_CONFIGS = {
+    # BASELINE configs[2] / [3] on one GPU: the pixels drawn
+    # in the band by the same generator (synthetic.draw_band), no files
+    'cfg3': dict(npc=(2, 2), dmax=200,
+                 workload='cfg3: the mouse genome at 10 kb, 20 mm10-sized '
+                          'chromosomes, 4 reps (2+2), dist_thresh_max 200, one '
+                          'genome-wide pooled estimate_disp + lrt'),
+    'cfg4': dict(npc=(6, 6, 6), dmax=400,
+                 workload='cfg4: human chr1 at 5 kb (49,792 bins), 18 reps '
+                          '(6+6+6), dist_thresh_max 400, estimate_disp + lrt '
+                          '(chi2 df 2)'),
+}
+
+
+def other_config(torch, ctx, dev, name, steps=2, warmup=1):
+    """One of the other north-star shapes through the bench's step
+    (estimate_disp + tables + lrt on HBM-resident inputs, as cfg2), timed on
+    this GPU after the headline measurement: `steps` steps after `warmup`,
+    kernel times from one extra profiled step."""
+    from hic3defdr_amd import synthetic
+    cfg = OTHER_CONFIGS[name]
+    bins = list(synthetic.MM10_BINS) if name == 'cfg3' else [49792]
+    t0 = time.perf_counter()
+    parts = synthetic.draw_genome(bins, cfg['npc'], cfg['dmax'], seed=0,
+                                  workers=16)
+    raw = np.concatenate([p[0] for p in parts])
+    f = np.concatenate([p[1] for p in parts])
+    dist_np = np.concatenate([p[2] for p in parts])
+    del parts
+    gen_s = time.perf_counter() - t0
+    n, R = raw.shape
+    C = len(cfg['npc'])
+    D = cfg['dmax'] + 1
+    cond = np.repeat(np.arange(C), cfg['npc']).astype(np.int32)
+    t_raw, t_f, t_dist = _upload(torch, dev, raw, f, dist_np)
+    present = np.isin(np.arange(D), dist_np)
+    del raw, f, dist_np
+    o = _outputs(torch, dev, n, C)
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    tl = table_lrt(torch, dev, ctx, D, C)
+
+    def step():
+        dpd = tl.estimate(t_raw, t_f, t_dist, n, R, cond)
+        tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
+        return dpd
+
+    first = None
+    for _ in range(warmup):
+        first = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        dpd = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    ctx.profile_reset()
+    ctx.profile(True, level=2)
+    step()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    ks = {k: ctx.profile_read(k)[0] for k in
+          ('disp_work', 'disp_nll', 'disp_update', 'disp_prep', 'lrt')}
+    p = o['p'].cpu().numpy()
+    ctx.set_stream(None)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    return {
+        'workload': cfg['workload'], 'bins': int(sum(bins)), 'reps': int(R),
+        'conds': int(C), 'disp_pixels': int(n), 'steps': steps,
+        'warmup': warmup, 'value': n * steps / el, 'unit': 'pixels/s',
+        'ms_per_step': el / steps * 1e3, 'kernels_ms_per_step': ks,
+        'generate_s': gen_s,
+        'checks': {
+            'disp_finite_where_present': bool(np.all(np.isfinite(
+                dpd[present]))),
+            'disp_nan_where_absent': bool(np.all(np.isnan(dpd[~present]))),
+            'p_in_0_1': bool(np.all((p >= 0) & (p <= 1))),
+            'deterministic_disp': None if first is None else bool(
+                np.array_equal(first, dpd, equal_nan=True))}}
+
+
 def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
     """Weak scaling: one 20k-bin chromosome per rank (BASELINE configs[1])."""
     import torch
@@ -692,6 +775,10 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
             out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
         if world == 1 and not args.no_e2e:
             out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
+        if world == 1 and not args.no_other_configs:
+            out['other_configs'] = {
+                name: other_config(torch, ctx, dev, name)
+                for name in ('cfg3', 'cfg4')}
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -828,6 +915,9 @@ def main():
                     help='runs of the full-chromosome CPU row (median)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--no-other-configs', action='store_true',
+                    help='skip the cfg3 / cfg4 lines measured after the '
+                         'headline (N = 1)')
     ap.add_argument('--noop-reduce', action='store_true',
                     help='measurement: run the multi-rank estimate_disp driver '
                          '(per-pass NLL sums through the reduce hook) on one '

@@ -9,7 +9,7 @@ vs=${1:-"base s"}
 first=${vs%% *}
 for rep in 1 2; do
 for v in $vs; do
-  H3D_LIB=$PWD/hic3defdr_amd/lib/variants/libh3d_$v.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-e2e --steps 10 \
+  H3D_LIB=$PWD/hic3defdr_amd/lib/variants/libh3d_$v.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-e2e --no-other-configs --steps 10 \
     > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
   python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').read().splitlines()[-1]); k=d['kernels_ms_per_step']; print('$v', round(d['value']/1e6,1), round(d['ms_per_step'],3), {a: round(b,3) for a, b in k.items() if a != 'note'})"
 done

@@ -7,7 +7,7 @@ tag=${1:-r}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 run() {
   timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/pmc_${tag}_$1 -o run -- \
-    python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e > gpurun_out/pmc_${tag}_$1.log 2>&1
+    python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-other-configs > gpurun_out/pmc_${tag}_$1.log 2>&1
 }
 run sq "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU"
 run f64 "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT"
