@@ -638,8 +638,12 @@ def other_config(torch, ctx, dev, name, steps=2, warmup=1):
     cfg = OTHER_CONFIGS[name]
     bins = list(synthetic.MM10_BINS) if name == 'cfg3' else [49792]
     t0 = time.perf_counter()
+    # (one chromosome: its replicates on the threads; the data do not depend
+    # on the thread count -- a seeded stream per replicate)
     parts = synthetic.draw_genome(bins, cfg['npc'], cfg['dmax'], seed=0,
-                                  workers=16)
+                                  workers=16) if len(bins) > 1 else \
+        [synthetic.draw_band(bins[0], cfg['npc'], cfg['dmax'], seed=0,
+                             chrom_index=0, workers=16)]
     raw = np.concatenate([p[0] for p in parts])
     f = np.concatenate([p[1] for p in parts])
     dist_np = np.concatenate([p[2] for p in parts])
