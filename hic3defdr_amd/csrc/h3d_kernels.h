@@ -388,12 +388,16 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
   const int lane = threadIdx.x & 63;
   const int64_t t0 = (int64_t)beg * kWv, t1 = (int64_t)end * kWv;
   const int64_t wt = (int64_t)gridDim.x * kWv;
-  const int64_t tdyn = t0 + ((t1 - t0) / wt) * static8 / 8 * wt;
+  // (fewer than two rounds of tasks: all dealt round-robin -- a wave does
+  // at most two, and the waves left without a task would otherwise each
+  // probe the 8 heads to find them empty)
+  const int64_t tdyn = (t1 - t0 < 2 * wt) ? t1 : t0 + ((t1 - t0) / wt) * static8 / 8 * wt;
   const int64_t tl = t1 - tdyn;
   int32_t* heads = meta + kTaskHeadStride * (1 + (PH == kEqualize ? 0 : 8));
   const int grp = blockIdx.x & 7;
   unsigned spent = 0u;
   auto take = [&]() -> int64_t {
+    if (tl <= 0) return t1;
 #pragma unroll 1
     for (int k = 0; k < 8; ++k) {
       const int p = (grp + k) & 7;
