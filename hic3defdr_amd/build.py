@@ -38,7 +38,7 @@ NATIVE_SRCS = [('h3d_api.hip', 'hipcc'), ('h3d_lrt.hip', 'hipcc'),
                ('h3d_bh.hip', 'hipcc'), ('h3d_table.hip', 'hipcc'),
                ('h3d_calls.cpp', 'g++'), ('h3d_npz.cpp', 'g++')]
 HEADERS = ['h3d_special.h', 'h3d_model.h', 'h3d_kernels.h', 'h3d_host.h',
-           'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h', 'h3d_lrt_group.h']
+           'h3d_prepare.h', 'h3d_errors.h', 'h3d_ctx.h', 'h3d_lrt_group.h', 'h3d_logtab.h']
 # concurrent compiles (each hipcc TU is single-threaded; the box sets
 # MAX_JOBS=16, this container has 8 CPUs)
 JOBS = max(1, min(int(os.environ.get('MAX_JOBS', '8')), os.cpu_count() or 1))

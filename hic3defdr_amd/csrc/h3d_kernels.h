@@ -842,8 +842,8 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
   // the NLL log's table in LDS: its lookup address depends on the value, so
   // the load sits on every lgamma's dependency chain (a global / L1 round
   // trip otherwise)
-  __shared__ LogTab s_tab[129];
-  for (int t = threadIdx.x; t < 129; t += kBrentBlock) s_tab[t] = kLogTab[t];
+  __shared__ LogTab s_tab[kLogTabLen];
+  for (int t = threadIdx.x; t < kLogTabLen; t += kBrentBlock) s_tab[t] = kLogTab[t];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   while (true) {
     __syncthreads();  // s_next / s_st reuse
@@ -978,8 +978,8 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
   __shared__ SegState s_st;
   __shared__ double wpart[kGangThreads / 64];
   __shared__ int s_next, s_more, s_abort;
-  __shared__ LogTab s_tab[129];  // the NLL log's table, as k_brent
-  for (int t = threadIdx.x; t < 129; t += kGangThreads) s_tab[t] = kLogTab[t];
+  __shared__ LogTab s_tab[kLogTabLen];  // the NLL log's table, as k_brent
+  for (int t = threadIdx.x; t < kLogTabLen; t += kGangThreads) s_tab[t] = kLogTab[t];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   while (true) {
     __syncthreads();  // s_next / s_st reuse
@@ -1111,8 +1111,8 @@ __global__ __launch_bounds__(kBlock) void k_lrt(
   for (int k = 0; k < M; ++k) cond[k] = (k < R) ? cond_of_rep[k] : -1;
   // the logpmf rows' log table in LDS (16 lookups per pixel at R = 4, each
   // on its term's dependency chain)
-  __shared__ LogTab s_tab[129];
-  for (int t = threadIdx.x; t < 129; t += blockDim.x) s_tab[t] = kLogTab[t];
+  __shared__ LogTab s_tab[kLogTabLen];
+  for (int t = threadIdx.x; t < kLogTabLen; t += blockDim.x) s_tab[t] = kLogTab[t];
   __syncthreads();
   int fl_all = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;

@@ -127,8 +127,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_lrt8(
   constexpr int J = M / kGroup;
   const int lane = threadIdx.x & (kGroup - 1);
   const int base = (threadIdx.x & 63) & ~(kGroup - 1);  // group's first lane
-  __shared__ LogTab s_tab[129];  // the rows' log table, as k_lrt
-  for (int t = threadIdx.x; t < 129; t += blockDim.x) s_tab[t] = kLogTab[t];
+  __shared__ LogTab s_tab[kLogTabLen];  // the rows' log table, as k_lrt
+  for (int t = threadIdx.x; t < kLogTabLen; t += blockDim.x) s_tab[t] = kLogTab[t];
   __syncthreads();
   int cnd[J];
 #pragma unroll

@@ -186,167 +186,37 @@ H3D_HD double hfma(double p, double x, double c) {
 #endif
 }
 
-// ln(m) for the NLL log: 129 buckets m_i = 1/2 + i/256 over frexp's
-// mantissa range [1/2, 1], c_i = 1/m_i rounded, l_i = ln(1/c_i) -- plus ln 2
-// for the buckets below sqrt(1/2) (i <= 53), whose exponent is taken one
-// lower, so ln x never cancels e ln 2 against ln m near x = 1 (x = 2^k lands
-// on c_0 = 2 exactly and returns (k - 1) ln 2 + 0). Entries: l_i correctly
-// rounded from 80-bit ln (tools/log_table.py).
+// ln(m) for the NLL log: kLogTabLen = 513 buckets m_i = 1/2 + i/1024 over
+// frexp's mantissa range [1/2, 1], c_i = 1/m_i rounded, l_i = ln(1/c_i) --
+// plus ln 2 for the buckets below sqrt(1/2) (i <= kLogTabShifted = 212),
+// whose exponent is taken one lower, so ln x never cancels e ln 2 against
+// ln m near x = 1 (x = 2^k lands on c_0 = 2 exactly and returns (k - 1) ln 2
+// + 0). Entries: l_i correctly rounded from 80-bit ln; generated into
+// h3d_logtab.h by tools/log_table.py. 8 KB: k_brent / k_lrt keep a copy in
+// LDS.
 struct LogTab {
   double c, l;
 };
-inline constexpr LogTab kLogTab[129] = {
-    {2.0, 0.0},
-    {1.9844961240310077, 0.007782140442054963},
-    {1.9692307692307693, 0.015504186535965199},
-    {1.9541984732824427, 0.023167059281534418},
-    {1.9393939393939394, 0.03077165866675366},
-    {1.9248120300751879, 0.03831886430213666},
-    {1.9104477611940298, 0.04580953603129422},
-    {1.8962962962962964, 0.05324451451881224},
-    {1.8823529411764706, 0.060624621816434854},
-    {1.8686131386861313, 0.06795066190850778},
-    {1.855072463768116, 0.07522342123758752},
-    {1.841726618705036, 0.08244366921107454},
-    {1.8285714285714285, 0.08961215868968717},
-    {1.8156028368794326, 0.09672962645855114},
-    {1.8028169014084507, 0.10379679368164355},
-    {1.7902097902097902, 0.11081436634029011},
-    {1.7777777777777777, 0.11778303565638351},
-    {1.7655172413793103, 0.12470347850095725},
-    {1.7534246575342465, 0.13157635778871932},
-    {1.7414965986394557, 0.1384023228591192},
-    {1.7297297297297298, 0.14518200984449783},
-    {1.7181208053691275, 0.151916042025842},
-    {1.7066666666666668, 0.15860503017663852},
-    {1.695364238410596, 0.16524957289530717},
-    {1.6842105263157894, 0.17185025692665928},
-    {1.673202614379085, 0.17840765747281825},
-    {1.6623376623376624, 0.18492233849401193},
-    {1.6516129032258065, 0.19139485299962947},
-    {1.641025641025641, 0.19782574332991992},
-    {1.6305732484076434, 0.20421554142869083},
-    {1.620253164556962, 0.21056476910734964},
-    {1.610062893081761, 0.2168739383006143},
-    {1.6, 0.2231435513142097},
-    {1.5900621118012421, 0.2293741010648459},
-    {1.5802469135802468, 0.23556607131276697},
-    {1.5705521472392638, 0.24171993688714513},
-    {1.5609756097560976, 0.2478361639045812},
-    {1.5515151515151515, 0.25391520998096345},
-    {1.5421686746987953, 0.259957524436926},
-    {1.532934131736527, 0.2659635484971379},
-    {1.5238095238095237, 0.2719337154836418},
-    {1.514792899408284, 0.2778684510034563},
-    {1.5058823529411764, 0.2837681731306446},
-    {1.4970760233918128, 0.2896332925830427},
-    {1.4883720930232558, 0.2954642128938359},
-    {1.4797687861271676, 0.30126133057816185},
-    {1.471264367816092, 0.3070250352949119},
-    {1.4628571428571429, 0.3127557100038969},
-    {1.4545454545454546, 0.3184537311185346},
-    {1.4463276836158192, 0.324119468654212},
-    {1.4382022471910112, 0.32975328637246804},
-    {1.4301675977653632, 0.3353555419211378},
-    {1.4222222222222223, 0.3409265869705932},
-    {1.4143646408839778, 0.3464667673462086},
-    {1.4065934065934067, -0.3411707574027672},
-    {1.3989071038251366, -0.33569129163814154},
-    {1.391304347826087, -0.3302416868705768},
-    {1.3837837837837839, -0.3248216194012377},
-    {1.3763440860215055, -0.3194307707663613},
-    {1.3689839572192513, -0.3140688276249758},
-    {1.3617021276595744, -0.30873548164961323},
-    {1.3544973544973544, -0.30343042941992004},
-    {1.3473684210526315, -0.2981533723190763},
-    {1.3403141361256545, -0.2929040164329327},
-    {1.3333333333333333, -0.28768207245178085},
-    {1.3264248704663213, -0.28248725557467697},
-    {1.3195876288659794, -0.27731928541623435},
-    {1.3128205128205128, -0.27217788591581565},
-    {1.3061224489795917, -0.26706278524904514},
-    {1.299492385786802, -0.2619737157415739},
-    {1.292929292929293, -0.2569104137850273},
-    {1.2864321608040201, -0.2518726197550701},
-    {1.28, -0.2468600779315258},
-    {1.2736318407960199, -0.2418725364204867},
-    {1.2673267326732673, -0.23690974707835774},
-    {1.2610837438423645, -0.23197146543777517},
-    {1.2549019607843137, -0.22705745063534608},
-    {1.248780487804878, -0.2221674653411543},
-    {1.2427184466019416, -0.2173012756899813},
-    {1.2367149758454106, -0.21245865121419336},
-    {1.2307692307692308, -0.20763936477824455},
-    {1.2248803827751196, -0.20284319251475144},
-    {1.2190476190476192, -0.19806991376209387},
-    {1.2132701421800949, -0.19331931100349606},
-    {1.2075471698113207, -0.18859116980754997},
-    {1.2018779342723005, -0.18388527877013738},
-    {1.1962616822429906, -0.17920142945771092},
-    {1.1906976744186046, -0.17453941635189965},
-    {1.1851851851851851, -0.16989903679539742},
-    {1.1797235023041475, -0.16528009093910292},
-    {1.1743119266055047, -0.16068238169047352},
-    {1.1689497716894977, -0.1561057146630616},
-    {1.1636363636363636, -0.15154989812720088},
-    {1.158371040723982, -0.14701474296180975},
-    {1.1531531531531531, -0.142500062607283},
-    {1.147982062780269, -0.1380056730194437},
-    {1.1428571428571428, -0.13353139262452257},
-    {1.1377777777777778, -0.12907704227514236},
-    {1.1327433628318584, -0.12464244520727659},
-    {1.1277533039647578, -0.12022742699815989},
-    {1.1228070175438596, -0.11583181552512165},
-    {1.1179039301310043, -0.11145544092532278},
-    {1.1130434782608696, -0.10709813555636712},
-    {1.1082251082251082, -0.10275973395776894},
-    {1.103448275862069, -0.09844007281325251},
-    {1.0987124463519313, -0.09413899091386191},
-    {1.0940170940170941, -0.08985632912186114},
-    {1.0893617021276596, -0.08559193033540353},
-    {1.0847457627118644, -0.0813456394539524},
-    {1.080168776371308, -0.0771173033444312},
-    {1.0756302521008403, -0.07290677080808773},
-    {1.0711297071129706, -0.06871389254805173},
-    {1.0666666666666667, -0.06453852113757116},
-    {1.062240663900415, -0.06038051098890748},
-    {1.0578512396694215, -0.05623971832287611},
-    {1.0534979423868314, -0.0521160011390141},
-    {1.0491803278688525, -0.04800921918636066},
-    {1.0448979591836736, -0.04391923393483558},
-    {1.0406504065040652, -0.03984590854719978},
-    {1.0364372469635628, -0.03578910785158529},
-    {1.032258064516129, -0.03174869831458027},
-    {1.0281124497991967, -0.02772454801485477},
-    {1.024, -0.023716526617316065},
-    {1.0199203187250996, -0.019724505347778573},
-    {1.0158730158730158, -0.015748356968139112},
-    {1.0118577075098814, -0.011787955752042173},
-    {1.0078740157480315, -0.007843177461025879},
-    {1.003921568627451, -0.003913899321136315},
-    {1.0, -0.0},
-};
-constexpr int kLogTabShifted = 53;  // buckets 0..53: m_i < sqrt(1/2)
+#include "h3d_logtab.h"
 
 // Natural log for finite x > 0, straight-line and table-driven:
-//   x = m 2^e, i = round(256 (m - 1/2)), t = m c_i - 1 (one fma, |t| <=
-//   2^-8), ln x = e' ln 2 + l_i + log1p(t), log1p by its degree-7 Taylor
-//   polynomial (truncation t^8 / 8 < 2^-67).
-// Max error 1.3e-16 absolute, 4.2e-16 relative (80-bit reference over
-// [1e-300, 1e300] and [0.3, 3]) at about two thirds of the instructions of
-// the atanh-series form it replaces (one reciprocal, 11 series terms). Used
-// by the NLL sums (finite x > 0 by construction) and, through
-// log_fast_checked, the incomplete-gamma prefactor.
-// (tab: the table's copy to read -- kLogTab, or k_brent's copy in LDS)
+//   x = m 2^e, i = round(1024 (m - 1/2)), t = m c_i - 1 (one fma, |t| <=
+//   2^-10), ln x = e' ln 2 + l_i + log1p(t), log1p by its degree-5 Taylor
+//   polynomial (truncation t^6 / 6 < 2^-62).
+// Max error 1.9e-16 absolute, 2.3e-16 relative (80-bit reference over
+// [1e-300, 1e300] (absolute 5.7e-14 there: |ln x| <= 690), [0.3, 3] and
+// [1, 1e4]). The 1024-step table (round 4; 256 steps and degree 7 before)
+// takes two fma off every log. Used by the NLL sums (finite x > 0 by
+// construction) and, through log_fast_checked, the incomplete-gamma
+// prefactor.
+// (tab: the table's copy to read -- kLogTab, or a kernel's copy in LDS)
 H3D_HD double log_fast(double x, const LogTab* tab = kLogTab) {
   int e;
   const double m = frexp(x, &e);  // [0.5, 1)
-  const int i = (int)((m - 0.5) * 256.0 + 0.5);  // 0..128
+  const int i = (int)((m - 0.5) * (double)kLogTabSteps + 0.5);  // 0..512
   const LogTab tb = tab[i];
   const double t = fma(m, tb.c, -1.0);
-  double q = 1.0 / 7.0;
-  q = hfma(q, t, -1.0 / 6.0);
-  q = hfma(q, t, 1.0 / 5.0);
+  double q = 1.0 / 5.0;
   q = hfma(q, t, -1.0 / 4.0);
   q = hfma(q, t, 1.0 / 3.0);
   q = hfma(q, t, -1.0 / 2.0);
