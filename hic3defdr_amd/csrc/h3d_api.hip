@@ -465,6 +465,7 @@ h3d_ctx* h3d_open(int device) {
   if (const char* e = std::getenv("H3D_NLL_W")) ctx->nll_w = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W8")) ctx->disp_w8 = std::atoi(e);
   if (const char* e = std::getenv("H3D_DISP_W2")) ctx->disp_w2 = std::atoi(e);
+  if (const char* e = std::getenv("H3D_PACK_GATHER")) ctx->pack_gather = std::atoi(e);
   if (const char* e = std::getenv("H3D_EQ_STATIC8"))
     ctx->eq_static8 = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("H3D_DISP_M2")) ctx->disp_m2 = std::atoi(e);
@@ -661,21 +662,40 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       // end_bit + 16 bits (cfg2: 24 bits, three radix passes)
       const int cbits = k32 ? 16 : 64 - end_bit;
       const int sort_bits = k32 ? end_bit + 16 : 64;
-      void* keys = scratch(ctx, "dkeys", n * (k32 ? 4 : 8));
+      // every condition of <= 2 replicates: one key pass for all of them,
+      // packed (raw, f) records for the gathers (k_dist_cond_keys_pack2)
+      const bool pack = k32 && maxnr <= 2 && ctx->pack_gather;
+      int32_t* d_nrep = nullptr;
+      CondPack2* packed = nullptr;
+      if (pack) {
+        d_nrep = (int32_t*)scratch(ctx, "sort_nrep", (size_t)C * 4);
+        packed = (CondPack2*)scratch(ctx, "cond_pack2", (size_t)C * n * sizeof(CondPack2));
+        if (!d_nrep || !packed) return fail(H3D_ENOMEM, "packed gather rows");
+        HIP_TRY(hipMemcpyAsync(d_nrep, nrep.data(), (size_t)C * 4, hipMemcpyHostToDevice, s));
+      }
+      void* keys = scratch(ctx, "dkeys", (pack ? (size_t)C : 1) * n * (k32 ? 4 : 8));
       void* keys_s = scratch(ctx, "dkeys_s", n * (k32 ? 4 : 8));
       if (!keys || !keys_s) return fail(H3D_ENOMEM, "sort keys");
       for (int c = 0; c < C; ++c) {
         const int32_t* reps_c = d_reps + c * kMaxReps;
-        if (k32) {
+        uint32_t* keys_c = pack ? (uint32_t*)keys + (size_t)c * n : (uint32_t*)keys;
+        if (pack) {
+          if (c == 0)
+            hipLaunchKernelGGL(k_dist_cond_keys_pack2, dim3(grid_for(ctx, n)), dim3(kBlock),
+                               0, s, d_dist, d_raw, d_f, n, R, C, d_reps, d_nrep, keys_c,
+                               packed);
+        } else if (k32) {
           hipLaunchKernelGGL(k_dist_cond_keys<uint32_t>, dim3(grid_for(ctx, n)),
                              dim3(kBlock), 0, s, d_dist, d_raw, n, R, reps_c, nrep[c],
-                             cbits, (uint32_t*)keys);
-          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)keys,
+                             cbits, keys_c);
+        }
+        if (k32) {
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_c,
                                                      (uint32_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, sort_bits, s));
           void* tmp = scratch(ctx, "cub_tmp", tmp_bytes);
           if (!tmp) return fail(H3D_ENOMEM, "sort temp");
-          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)keys,
+          HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys_c,
                                                      (uint32_t*)keys_s, idx_in, idx_out,
                                                      (int)n, 0, sort_bits, s));
           if (c == 0)
@@ -702,6 +722,11 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
           const int r = rep_idx[(size_t)c * kMaxReps + j];
           rows.raw[j] = raw_s + (size_t)r * n;
           rows.f[j] = f_s + (size_t)r * n;
+        }
+        if (pack) {
+          hipLaunchKernelGGL(k_gather_pack2, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s,
+                             idx_out, packed + (size_t)c * n, n, nrep[c], rows);
+          continue;
         }
         const int64_t tiles = (n + kGatherTile - 1) / kGatherTile;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)ctx->n_cu * 8));

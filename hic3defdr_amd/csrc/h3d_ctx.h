@@ -115,6 +115,10 @@ struct h3d_ctx {
   // k_disp_work: eighths of the task rounds dealt statically (the rest from
   // a device counter); H3D_EQ_STATIC8
   int eq_static8 = 4;
+  // H3D_PACK_GATHER: a condition of <= 2 replicates gathers from a 32-byte
+  // packed copy of its replicates' (raw, f) written by the key pass (one
+  // sector per pixel instead of a raw and an f line)
+  int pack_gather = 1;
   int disp_m2 = 1;
   // H3D_BRENT: 1 = gang Brent searches (k_brent_gang) where one workgroup
   // per segment leaves CUs idle, 2 = always, 0 = k_brent only

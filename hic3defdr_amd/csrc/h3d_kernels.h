@@ -209,6 +209,68 @@ __global__ void k_dist_cond_keys(const int32_t* __restrict__ dist,
   }
 }
 
+// k_dist_cond_keys for every condition at once when each has <= 2
+// replicates (32-bit keys): one streaming pass over the pixels' raw and f
+// rows writes condition c's keys (keys + c n) and its (raw, f) of each pixel
+// as one 32-byte record (packed + c n) for k_gather_pack2 -- the gather
+// through the condition's sort order then touches one 32-byte sector per
+// pixel instead of a line of the raw rows and a line of the f rows.
+// reps: kMaxReps entries per condition, as the per-condition pass.
+struct alignas(32) CondPack2 {
+  int32_t raw[4];  // [0, nr) used
+  double f[2];
+};
+
+static __global__ void k_dist_cond_keys_pack2(const int32_t* __restrict__ dist,
+                                              const int32_t* __restrict__ raw,
+                                              const double* __restrict__ f, int64_t n,
+                                              int R, int C, const int32_t* __restrict__ reps,
+                                              const int32_t* __restrict__ nrep,
+                                              uint32_t* __restrict__ keys,
+                                              CondPack2* __restrict__ packed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t d = (uint32_t)dist[i];
+    if (d > 0xffffu) d = 0xffffu;
+    for (int c = 0; c < C; ++c) {
+      const int r0 = reps[c * kMaxReps], r1 = nrep[c] > 1 ? reps[c * kMaxReps + 1] : r0;
+      const uint32_t v0 = (uint32_t)raw[i * R + r0], v1 = (uint32_t)raw[i * R + r1];
+      const uint64_t mx = v0 > v1 ? v0 : v1, mn = v0 < v1 ? v0 : v1;
+      keys[c * n + i] = (uint32_t)((d << 16) | (count_code8(mn) << 8) | count_code8(mx));
+      int4 rv;
+      rv.x = (int)v0;
+      rv.y = (int)v1;
+      rv.z = 0;
+      rv.w = 0;
+      double2 fv;
+      fv.x = f[i * R + r0];
+      fv.y = f[i * R + r1];
+      int4* q = reinterpret_cast<int4*>(packed + c * n + i);
+      q[0] = rv;
+      reinterpret_cast<double2*>(q + 1)[0] = fv;
+    }
+  }
+}
+
+// The gather of one condition (<= 2 replicates) through its sort order from
+// the packed records: dst rows j < nr of pixel i = record perm[i].
+static __global__ void k_gather_pack2(const int32_t* __restrict__ perm,
+                                      const CondPack2* __restrict__ packed, int64_t n,
+                                      int nr, SoaRows dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int4* q = reinterpret_cast<const int4*>(packed + perm[i]);
+    const int4 rv = q[0];
+    const double2 fv = reinterpret_cast<const double2*>(q + 1)[0];
+    dst.raw[0][i] = rv.x;
+    dst.f[0][i] = fv.x;
+    if (nr > 1) {
+      dst.raw[1][i] = rv.y;
+      dst.f[1][i] = fv.y;
+    }
+  }
+}
+
 // sort key (distance, total count capped to cbits bits): inside a distance
 // segment pixels of similar depth sit in the same wave, so the q2qnbinom
 // branches (tail side, series vs continued fraction) diverge less. The count
