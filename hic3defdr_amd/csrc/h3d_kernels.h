@@ -473,6 +473,12 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
     }
     return t1;
   };
+  // the table log's table in LDS (the equalize pass's logs: the prefactor of
+  // every incomplete-gamma evaluation, lgamma of the shapes, the mean MLE's
+  // start, log f): a per-lane global load sat on each one's chain
+  __shared__ LogTab s_tab[kLogTabLen];
+  for (int k = threadIdx.x; k < kLogTabLen; k += kBlock) s_tab[k] = kLogTab[k];
+  __syncthreads();
   int64_t t = t0 + (int64_t)blockIdx.x * kWv + (threadIdx.x >> 6);
   if (t >= tdyn) t = take();
   for (; t < t1; t = (t + wt < tdyn) ? t + wt : take()) {
@@ -502,12 +508,12 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           const bool on = k < nr;
           x[k] = on ? (double)raw_s[(int64_t)ri[k] * n + px] : 0.0;
           f[k] = on ? f_s[(int64_t)ri[k] * n + px] : 1.0;
-          lf[k] = on ? log_fast_checked(f[k]) : 0.0;
+          lf[k] = on ? log_fast_checked(f[k], s_tab) : 0.0;
           as[k] = alpha;
         }
         int fl = 0;
         const double f_mean = exp_fast(np_sum<MS>(lf, nr) / nr) - 0.0;
-        const double mu = fit_mu<MS>(x, f, as, nr, ~0u, &fl);
+        const double mu = fit_mu<MS>(x, f, as, nr, ~0u, &fl, s_tab);
         if (fl) atomicOr(&seg_flags[s], fl);
         const double mu_out0 = mu * f_mean;
         // The reference clamps (mu_in, mu_out) to 0.25 in place and carries
@@ -544,7 +550,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           const int64_t o = (int64_t)ri[k] * n + px;
           double mu_in = mu * f_s[o];
           double mu_out = (k > fc) ? 0.25 : mu_out0;
-          pd[o] = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache);
+          pd[o] = q2q((double)raw_s[o], &mu_in, &mu_out, alpha, &cache, s_tab);
         }
       }
       if constexpr (!NLL) continue;
@@ -563,11 +569,11 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           const double dk = d[0];
 #pragma unroll
           for (int j = 0; j + 1 < MS; ++j) d[j] = d[j + 1];
-          lgsum += lgam_nll(dk + kc.r);
+          lgsum += lgam_nll(dk + kc.r, s_tab);
           z += dk;
         }
       }
-      term = lgsum + kc.lg_nr - lgam_nll(z + kc.nr) - kc.n_lg_r;
+      term = lgsum + kc.lg_nr - lgam_nll(z + kc.nr, s_tab) - kc.n_lg_r;
     } else if (M >= 8 && i < chunk_len[chunk]) {
       // >= 8 replicates in the condition: numpy's pairwise row sums
       const int64_t px = chunk_start[chunk] + i;
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
             f[k] = 1.0;
           }
         }
-        const int fl = equalize_pixel<M>(x, f, nr, st[s].disp, d);
+        const int fl = equalize_pixel<M>(x, f, nr, st[s].disp, d, s_tab);
         if (fl) atomicOr(&seg_flags[s], fl);
 #pragma unroll
         for (int k = 0; k < M; ++k)
@@ -599,7 +605,7 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
           d[k] = (k < nr) ? pd[(int64_t)ri[k] * n + px] : 0.0;
       }
       const NllConst kc = st[s].k;
-      term = nll_pixel<M>(d, nr, kc);
+      term = nll_pixel<M>(d, nr, kc, s_tab);
     }
     // one partial per wave (fixed shuffle tree -> deterministic); no block
     // barrier, so the waves of a block run their items independently

@@ -101,7 +101,7 @@ struct NpSumStream {
 // safeguard), to full double precision.
 template <int M, typename TX>
 H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
-                     unsigned mask, int* status) {
+                     unsigned mask, int* status, const LogTab* tab = kLogTab) {
   double sx = 0.0, sb = 0.0;
   bool bad = false;
 #pragma unroll
@@ -127,7 +127,7 @@ H3D_HD double fit_mu(const TX* x, const double* b, const double* a, int n,
   // start is closer to it (wave of 64 pixels: 2.37 against 2.62 steps)
   // (the table log and straight-line exp of h3d_special.h: ~1 ulp, the
   // OCML forms carried constant copies; the MLE is Newton-converged anyway)
-  double th = log_fast_checked(div_fast(sx, sb));
+  double th = log_fast_checked(div_fast(sx, sb), tab);
   double lo = -INFINITY, hi = INFINITY;
   for (int it = 0; it < 200; ++it) {
     H3D_STAT(fit_it, 1);
@@ -243,13 +243,13 @@ struct LgamCache {
 // the incomplete-gamma prefactor by the same relative amount). cephes lgam's
 // shift loop below 13 with an IEEE division per step serialised the lanes of
 // a wave (gfx950 r03 asm: two divergent loops per call).
-H3D_HD double lgam_q2q(double a) { return lgam_nll(a); }
+H3D_HD double lgam_q2q(double a, const LogTab* tab = kLogTab) { return lgam_nll(a, tab); }
 
-H3D_HD double lgam_cached(double a, LgamCache* c) {
-  if (!c) return lgam_q2q(a);
+H3D_HD double lgam_cached(double a, LgamCache* c, const LogTab* tab = kLogTab) {
+  if (!c) return lgam_q2q(a, tab);
   if (a != c->a) {
     c->a = a;
-    c->lga = lgam_q2q(a);
+    c->lga = lgam_q2q(a, tab);
   }
   return c->lga;
 }
@@ -258,19 +258,19 @@ H3D_HD double lgam_cached(double a, LgamCache* c) {
 // output gamma shape either given (lga_out) or taken from `cache` (lga_out
 // NaN).
 H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
-                       double lga_out, LgamCache* cache);
+                       double lga_out, LgamCache* cache, const LogTab* tab = kLogTab);
 
 H3D_HD double q2q(double x, double* mu_in, double* mu_out, double alpha,
-                  LgamCache* cache = nullptr) {
+                  LgamCache* cache = nullptr, const LogTab* tab = kLogTab) {
   if (!((*mu_in >= 0.25) && (*mu_out >= 0.25))) {
     *mu_in = 0.25;
     *mu_out = 0.25;
   }
-  return q2q_core(x, *mu_in, *mu_out, alpha, NAN, cache);
+  return q2q_core(x, *mu_in, *mu_out, alpha, NAN, cache, tab);
 }
 
 H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
-                       double lga_out, LgamCache* cache) {
+                       double lga_out, LgamCache* cache, const LogTab* tab) {
   // (the quotients here by div_fast: ~1 ulp on gfx950 instead of the IEEE
   // division sequence; the q2q values move by rounding only, test bar 1e-10)
   const double r_in = 1 + alpha * mi, r_out = 1 + alpha * mo;
@@ -305,7 +305,7 @@ H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
     tg = right ? 1.0 : 0.0;
   } else {
     double P, Q, fac;
-    igam_pq(a_in, xs, lgam_q2q(a_in), &P, &Q, &fac, right ? 1 : 0);
+    igam_pq(a_in, xs, lgam_q2q(a_in, tab), &P, &Q, &fac, right ? 1 : 0, tab);
     tg = right ? Q : P;
   }
   double qg;
@@ -337,8 +337,8 @@ H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
 #endif
       if (y > 0.0) guess = a_out * y * y * y;
     }
-    const double lga = (lga_out == lga_out) ? lga_out : lgam_cached(a_out, cache);
-    qg = igam_inv(a_out, tg, right, lga, guess) * r_out;
+    const double lga = (lga_out == lga_out) ? lga_out : lgam_cached(a_out, cache, tab);
+    qg = igam_inv(a_out, tg, right, lga, guess, tab) * r_out;
   }
   double pc = (qn + qg) / 2;
   if (!(pc >= 0.0)) pc = 0.0;
@@ -349,24 +349,24 @@ H3D_HD double q2q_core(double x, double mi, double mo, double alpha,
 // x, f: the condition's n replicates (compacted, in design order).
 template <int M>
 H3D_HD int equalize_pixel(const double* x, const double* f, int n, double alpha,
-                          double* out) {
+                          double* out, const LogTab* tab = kLogTab) {
   double lf[M], as[M];
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    lf[k] = (k < n) ? log_fast_checked(f[k]) : 0.0;
+    lf[k] = (k < n) ? log_fast_checked(f[k], tab) : 0.0;
     as[k] = alpha;
   }
   // gmean(f, pseudocount=0, axis=1) = exp(nanmean(log f)) - 0
   const double f_mean = exp_fast(np_sum<M>(lf, n) / n) - 0.0;
   int st = 0;
-  const double mu = fit_mu<M>(x, f, as, n, ~0u, &st);
+  const double mu = fit_mu<M>(x, f, as, n, ~0u, &st, tab);
   double mu_out = mu * f_mean;
   LgamCache cache;
 #pragma unroll
   for (int k = 0; k < M; ++k)
     if (k < n) {
       double mu_in = mu * f[k];
-      out[k] = q2q(x[k], &mu_in, &mu_out, alpha, &cache);
+      out[k] = q2q(x[k], &mu_in, &mu_out, alpha, &cache, tab);
     }
   return st;
 }

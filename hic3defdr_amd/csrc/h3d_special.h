@@ -305,7 +305,7 @@ H3D_HD double rise5(double x) {
 // factorial x (x+1) (x+2) (x+3) (x+4) = ((((x + 10) x + 35) x + 50) x + 24) x
 // (positive coefficients: no cancellation for x > 0), y lands in [10, 15).
 // FMA contraction is on here: only the absolute error matters (see above).
-H3D_HD double lgam_nll(double x) {
+H3D_HD double lgam_nll(double x, const LogTab* tab = kLogTab) {
 #if defined(__clang__)
 #pragma clang fp contract(fast)
 #endif
@@ -322,8 +322,8 @@ H3D_HD double lgam_nll(double x) {
   }
   const double r = recip_nll(y), r2 = r * r;
   const double corr = r * stirling_nll(r2);
-  double v = (y - 0.5) * log_fast(y) - y + kLogSqrt2Pi + corr;
-  if (x < 10.0) v -= log_fast(P);
+  double v = (y - 0.5) * log_fast(y, tab) - y + kLogSqrt2Pi + corr;
+  if (x < 10.0) v -= log_fast(P, tab);
   return v;
 }
 
@@ -454,15 +454,15 @@ H3D_HD double stirling_corr(double a) {
 // x^a e^-x / Gamma(a), given lga = lgam(a).
 // (table-driven log_fast / straight-line exp_fast: the exponent's own
 // conditioning, a few ulp of |a ln x|, dominates their <= 1 ulp)
-H3D_HD double igam_fac_l(double a, double x, double lga) {
+H3D_HD double igam_fac_l(double a, double x, double lga, const LogTab* tab = kLogTab) {
   if (fabs(a - x) > 0.4 * fabs(a) || a < 10.0) {
-    double ax = a * log_fast_checked(x) - x - lga;
+    double ax = a * log_fast_checked(x, tab) - x - lga;
     if (ax < -kMaxLog) return 0.0;
     return exp_fast(ax);
   }
   H3D_STAT(fac_l1, 1);
   double s = (x - a) / a;
-  return exp_fast(a * log1pmx(s) + 0.5 * log_fast_checked(a / kTwoPi) - stirling_corr(a));
+  return exp_fast(a * log1pmx(s) + 0.5 * log_fast_checked(a / kTwoPi, tab) - stirling_corr(a));
 }
 
 H3D_HD double igam_fac(double a, double x) { return igam_fac_l(a, x, lgam(a)); }
@@ -619,9 +619,9 @@ H3D_HD double igamc_cf(double a, double x) {
 // x < 1.5 a + 5 -- instead of cephes' x-vs-a switch, so lanes of a wave that
 // want the same tail take the same branch. tail = -1: the cephes rule.
 H3D_HD void igam_pq(double a, double x, double lga, double* P, double* Q,
-                    double* fac, int tail = -1) {
+                    double* fac, int tail = -1, const LogTab* tab = kLogTab) {
   H3D_STAT(pq, 1);
-  const double f = igam_fac_l(a, x, lga);
+  const double f = igam_fac_l(a, x, lga, tab);
   *fac = f;
   // v = the directly computed tail, is_q = whether it is Q; P and Q are then
   // written once, by selects (per-branch stores through P / Q made the
@@ -949,7 +949,7 @@ H3D_HD void igam_step_taylor(double a, double xe, double h, double* dint,
 // (~1e-4 relative) thus takes ONE incomplete-gamma evaluation: the confirming
 // Halley step runs on the continuation.
 H3D_HD double igam_inv(double a, double t, bool upper, double lga,
-                       double guess = -1.0) {
+                       double guess = -1.0, const LogTab* tab = kLogTab) {
   H3D_STAT(inv, 1);
   H3D_STAT(wh, guess > 0.0);
   if (t > 0.9) {
@@ -973,7 +973,7 @@ H3D_HD double igam_inv(double a, double t, bool upper, double lga,
       dP = dPe * ratio;
     } else {
       double P, Q, fac;
-      igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0);
+      igam_pq(a, x, lga, &P, &Q, &fac, upper ? 1 : 0, tab);
       if (fac == 0.0) return x;
       F = (upper ? Q : P) - t;
       dP = fac / x;
