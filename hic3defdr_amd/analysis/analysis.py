@@ -328,8 +328,8 @@ class AnalyzingHiC3DeFDR(object):
                              t_dist.data_ptr() if n else None, n,
                              t_disp.data_ptr() if n else None)
         # (table_gather_dev returns with the ctx stream drained); the per-pixel
-        # disp goes to the outdir by a stream-ordered copy into pinned memory
-        # that lands behind the LRT (analysis/d2h.py)
+        # disp goes to the outdir by a copy into pageable host memory on a
+        # background thread (analysis/d2h.py; pinning measured slower there)
         tables = t_tab.cpu().numpy()
         disp, disp_ready = to_host_async(t_disp)
         del t_disp

@@ -517,11 +517,15 @@ H3D_HD double stirling_corr(double a) {
 // (table-driven log_fast / straight-line exp_fast: the exponent's own
 // conditioning, a few ulp of |a ln x|, dominates their <= 1 ulp)
 H3D_HD double igam_fac_l(double a, double x, double lga, const LogTab* tab = kLogTab) {
-  // the plain exponent below a = 50 (the log1pmx form is for the
-  // cancellation of a ln x - x - lgamma(a) at large a near x: below 50 its
-  // rounding, ~2e-16 x |a ln x|, is inside the prefactor's own conditioning
-  // -- the unit grids' bar -- and the wave does not split over the two forms
-  // at a ~ 10..20, the equalize pass' common shapes)
+  // the plain exponent below a = 50, a deliberate speed-for-accuracy trade:
+  // near x ~ a the exponent a ln x - x - lgamma(a) cancels (its derivatives
+  // in a and x vanish at the mode, so the prefactor itself is well
+  // conditioned there) and its rounding, ~2e-16 x |a ln x|, becomes relative
+  // error of the prefactor -- measured up to 8e-14 at a in [10, 50) against
+  // 2.8e-14 for cephes' log1pmx form above 50 (test_special_host.py::
+  // test_igam_plain_prefactor_near_the_mode pins both). It stays far inside
+  // the equalize pass' 1e-10 bar, and the wave no longer splits over the two
+  // forms at a ~ 10..20, the equalize pass' common shapes (r05s: -1 %).
   if (fabs(a - x) > 0.4 * fabs(a) || a < 50.0) {
     double ax = a * log_fast_checked(x, tab) - x - lga;
     if (ax < -kMaxLog) return 0.0;

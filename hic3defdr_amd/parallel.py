@@ -145,7 +145,9 @@ def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
     dist.all_to_all_single(recv, send.to(xdev), group=group)
     s_list, r_list = send.tolist(), recv.tolist()
     m = int(sum(r_list))
-    k = max(1, int(chunks)) if n or m else 1
+    # every rank issues the same number of collectives, pixels or not (a
+    # rank with n == m == 0 sends and receives empty parts)
+    k = max(1, int(chunks))
     cols = [as_bytes(t_raw, 4 * R), as_bytes(t_f, 8 * R), as_bytes(t_dist, 4)]
     s_off = np.concatenate([[0], np.cumsum(s_list)])
     r_off = np.concatenate([[0], np.cumsum(r_list)])

@@ -376,7 +376,7 @@ def test_bh_sharded_equals_single_process(world):
     np.testing.assert_array_equal(got, want)
 
 
-def _exchange_worker(rank, world, port, result_file):
+def _exchange_worker(rank, world, port, result_file, idle=False):
     import torch
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -388,7 +388,8 @@ def _exchange_worker(rank, world, port, result_file):
     raw = torch.from_numpy(rng.integers(0, 1000, (n, R)).astype(np.int32))
     f = torch.from_numpy(rng.random((n, R)))
     d = torch.from_numpy(rng.integers(0, 60, n).astype(np.int32))
-    owner = torch.from_numpy(rng.integers(0, world, n).astype(np.int64))
+    owner = torch.from_numpy(
+        rng.integers(0, world - int(idle), n).astype(np.int64))
     outs = []
     for chunks in (1, 3, 7):
         outs.append([t.numpy().copy() for t in parallel.exchange_by_owner(
@@ -398,18 +399,21 @@ def _exchange_worker(rank, world, port, result_file):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 3])
-def test_chunked_reshard_equals_one_shot(world):
+@pytest.mark.parametrize('world,idle', [(2, False), (3, False), (2, True),
+                                        (3, True)])
+def test_chunked_reshard_equals_one_shot(world, idle):
     """parallel.exchange_by_owner (the distance re-shard's all_to_all): cut
     into 3 or 7 asynchronous parts, every rank receives exactly what the
     one-shot exchange gives it, bit for bit -- and that is every source
     rank's pixels owned by this rank, source by source in their order (the
-    last rank sends nothing)."""
+    last rank sends nothing; with ``idle`` it also owns nothing, so it has
+    no pixel either way and must still take part in every part's
+    collective)."""
     with tempfile.TemporaryDirectory() as tmp:
         res = os.path.join(tmp, 'x_%d.npz')
-        port = 29900 + (os.getpid() % 1000) + world
-        mp.spawn(_exchange_worker, args=(world, port, res), nprocs=world,
-                 join=True)
+        port = 29900 + (os.getpid() % 1000) + world + 10 * int(idle)
+        mp.spawn(_exchange_worker, args=(world, port, res, idle),
+                 nprocs=world, join=True)
         srcs = []
         for r in range(world):
             rng = np.random.default_rng(100 + r)
@@ -417,7 +421,7 @@ def test_chunked_reshard_equals_one_shot(world):
             raw = rng.integers(0, 1000, (n, 4)).astype(np.int32)
             f = rng.random((n, 4))
             d = rng.integers(0, 60, n).astype(np.int32)
-            owner = rng.integers(0, world, n)
+            owner = rng.integers(0, world - int(idle), n)
             srcs.append((raw, f, d, owner))
         for r in range(world):
             z = np.load(res % r)
