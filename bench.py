@@ -35,6 +35,21 @@ analysis.py:247-257) on a 1,000-bin sample -- its O(fail * N) cost grows
 super-linearly with the chromosome, so the survey's own measurement of the
 reference at cfg2 is quoted beside it.
 
+The north star's headline shape, cfg3 (the whole mouse genome), is measured
+beside the cfg2 line at N = 1 (other_configs.cfg3): the genome is drawn once
+before the GPU is touched, the fallback-fixed restatement runs estimate_disp +
+lrt over all of it ONCE on every allowed core (other_configs.cfg3.
+cpu_baseline, with gpu_over_cpu), and after the GPU's timed steps on the same
+genome every pixel's p, the genome-wide BH calls at FDR 0.01 / 0.05 / 0.1 and
+the segments beyond 1e-6 are compared (vs_cpu_restatement, identical_calls).
+e2e_cfg3_run_to_qvalues: the same shape END TO END from files through the
+class (the genome written in the reference's layout before the GPU starts).
+
+Roofline denominators: the spec peaks and this GPU's measured ones
+(measured_peaks: FP64 FMA chains and a 16 B/lane copy, libh3d_peak.so, run
+before the headline); the dominant kernel's launch time from the live HIP
+events and from the committed rocprofv3 stats of the same command.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -55,7 +70,15 @@ METRIC = ("pixels/sec through estimate_disp+lrt, 4 reps @10kb; "
           "max-|Δq| vs reference")
 
 PMC_SUMMARY = os.path.join(REPO, 'profiles', 'pmc_default.json')
-FP64_PEAK_TFLOPS = 78.6   # MI355X vector FP64, dense (MI355X_MICROARCH.md)
+# rocprofv3 --kernel-trace --stats of the same default command (the kernel
+# durations the committed PMC summary is read against)
+KSTATS = os.path.join(REPO, 'profiles', 'kernel_stats_default.json')
+# spec peaks: FP64 vector 78.6 TFLOP/s is AMD's MI355X product figure (dense,
+# no sparsity; MI355X_MICROARCH.md gives no FP64 number); HBM3E 8.0 TB/s spec
+# (MI355X_MICROARCH.md: 6.29 TB/s measured with a float4 copy). The bench
+# measures both on the box before the headline (measured_peaks,
+# libh3d_peak.so) and reports every fraction against both.
+FP64_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 CPU_RUNS = 4
 
@@ -123,12 +146,73 @@ def pmc_kernel(kernel, bins, dmax):
             'active_insts': acc['SQ_ACTIVE_INST_VALU']}
 
 
+def measured_peaks(device):
+    """The box's own roofline denominators (csrc/h3d_peak.hip): independent
+    v_fma_f64 chains at 8 waves per SIMD on every CU, and a 16 B/lane
+    streaming copy of 2 GiB (read + write bytes), each the best of 10 timed
+    launches after a warm-up. None when libh3d_peak.so is absent."""
+    import ctypes
+    from hic3defdr_amd import build as h3dbuild
+    path = os.path.join(h3dbuild.LIBDIR, 'libh3d_peak.so')
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    buf = (ctypes.c_double * 4)()
+    st = lib.h3d_peak_fp64(device, 10, buf)
+    fp64 = {'best_tflops': buf[0], 'median_tflops': buf[1],
+            'flops_per_launch': buf[2], 'best_ms': buf[3],
+            'kernel': 'k_fma_chains: 8 independent v_fma_f64 chains x 16 '
+                      'unrolled x 2048 trips per lane, 8 waves per SIMD, '
+                      'every CU'} if st == 0 else {'error': st}
+    st = lib.h3d_peak_copy(device, ctypes.c_int64(1 << 30), 10, buf)
+    hbm = {'best_gbs': buf[0], 'median_gbs': buf[1],
+           'bytes_per_launch': buf[2], 'best_ms': buf[3],
+           'kernel': 'k_copy16: double2 load + store per lane, grid-stride, '
+                     '1 GiB -> 1 GiB, 16 waves per CU; read + write bytes'} \
+        if st == 0 else {'error': st}
+    return {'fp64': fp64, 'hbm': hbm, 'source': 'bench.py measured_peaks '
+            '(hic3defdr_amd/csrc/h3d_peak.hip), run on this GPU before the '
+            'headline'}
+
+
+def _peak(peaks, kind):
+    try:
+        return peaks[kind]['best_tflops' if kind == 'fp64' else 'best_gbs']
+    except (TypeError, KeyError):
+        return None
+
+
+def rocprof_avg_us(kernel, bins, dmax):
+    """Average launch duration of `kernel` (name prefix) in the committed
+    rocprofv3 --kernel-trace --stats summary of the default command, or None
+    unless the workload is the one it was measured on."""
+    import csv
+    try:
+        meta = json.load(open(KSTATS))
+    except (OSError, ValueError):
+        return None
+    if meta.get('bins') != bins or meta.get('dmax') != dmax:
+        return None
+    calls = tot = 0
+    with open(os.path.join(REPO, meta['csv'])) as fh:
+        for row in csv.DictReader(fh):
+            # 'void h3d::k_disp_work<2, 4, 0, false>(int const*, ...)'
+            name = row['Name'].split('(')[0].strip()
+            if name.endswith(kernel):
+                calls += int(row['Calls'])
+                tot += float(row['TotalDurationNs'])
+    if not calls:
+        return None
+    return {'avg_us': tot / calls / 1e3, 'calls': calls,
+            'source': meta['csv'], 'command': meta.get('command')}
+
+
 def bytes_per_lrt_pixel(R, C):
     # raw int32 4R + f 8R + dist 4 in; p, llr, mu0 24 + mu1 8C + disp 8C out
     return 12 * R + 16 * C + 28
 
 
-def fp64_roof(pmc, avg_s):
+def fp64_roof(pmc, avg_s, peak_measured=None):
     if not pmc or not avg_s:
         return None
     ach = pmc['f64_flops'] / avg_s / 1e12
@@ -136,6 +220,9 @@ def fp64_roof(pmc, avg_s):
            'frac': ach / FP64_PEAK_TFLOPS,
            'flops_per_launch': pmc['f64_flops'],
            'lane_util': pmc['lane_util']}
+    if peak_measured:
+        out['peak_measured'] = peak_measured
+        out['frac_measured'] = ach / peak_measured
     if pmc['lane_util'] is not None:
         out['useful_frac'] = out['frac'] * pmc['lane_util']
     return out
@@ -157,34 +244,52 @@ def _lrt_task(args):
     return oracle.lrt(raw, f, dw, design, faithful=faithful)[0]
 
 
-def cpu_pipeline(pool, workers, raw, f, dist, design, D, faithful):
+def cpu_pipeline(pool, workers, raw, f, dist, design, D, faithful,
+                 with_table=False, progress=False):
     """estimate_disp + lrt on the CPU with the reference's parallel structure:
     qcml per (distance, condition) over the pool (analysis.py:193-200), the
     lowess fit per condition, then the LRT -- faithful: one call over the
     chromosome (one process per chromosome, analysis.py:247-257);
-    fallback-fixed: pixel blocks over the pool. Returns p."""
+    fallback-fixed: pixel blocks over the pool. Returns p (and the (D, C)
+    disp_per_dist with ``with_table``)."""
     import oracle
     C = design.shape[1]
     order = np.argsort(dist, kind='stable')
     bounds = np.searchsorted(dist[order], np.arange(D + 1))
-    tasks = []
-    for c in range(C):
-        cols = design[:, c]
-        for d in range(D):
-            sel = order[bounds[d]:bounds[d + 1]]
-            tasks.append((raw[sel][:, cols], f[sel][:, cols], faithful))
-    dpd = np.array(pool.map(_qcml_task, tasks, chunksize=4)).reshape(C, D).T
+    def tasks():
+        for c in range(C):
+            cols = design[:, c]
+            for d in range(D):
+                sel = order[bounds[d]:bounds[d + 1]]
+                yield raw[sel][:, cols], f[sel][:, cols], faithful
+    # largest segments first would shorten the pool's tail, but the results
+    # must come back in (condition, distance) order: imap keeps it
+    def beat(it, what):
+        # a progress line on stderr every ~30 s (long legs: the cfg3 genome)
+        t = time.perf_counter()
+        for k, v in enumerate(it):
+            if progress and time.perf_counter() - t > 30:
+                t = time.perf_counter()
+                print('bench: cpu %s %d ...' % (what, k), file=sys.stderr,
+                      flush=True)
+            yield v
+    dpd = np.array(list(beat(pool.imap(_qcml_task, tasks(), chunksize=2),
+                             'segments'))).reshape(C, D).T
     disp = np.zeros((len(raw), C))
     for c in range(C):
         fin = np.isfinite(dpd[:, c])
         x, y = np.arange(D)[fin], dpd[fin, c]
         disp[:, c] = oracle.weighted_lowess_fit(x, y, left_boundary=y[0])(dist)
     dw = np.dot(disp, design.T)
+    del disp
     if faithful:
-        return _lrt_task((raw, f, dw, design, True))
-    blocks = np.array_split(np.arange(len(raw)), workers * 4)
-    return np.concatenate(pool.map(
-        _lrt_task, [(raw[b], f[b], dw[b], design, False) for b in blocks]))
+        p = _lrt_task((raw, f, dw, design, True))
+    else:
+        blocks = np.array_split(np.arange(len(raw)), workers * 4)
+        p = np.concatenate(list(beat(pool.imap(
+            _lrt_task, ((raw[b], f[b], dw[b], design, False) for b in blocks)),
+            'lrt blocks')))
+    return (p, dpd) if with_table else p
 
 
 # SURVEY.md §6 [probe]: the reference itself on cfg2 (20k bins, dmax 250;
@@ -281,13 +386,7 @@ def cpu_baseline_run(full_bins, sample_bins, dmax, seed=123, full_runs=1):
     import multiprocessing
     import oracle
     ncpu = os.cpu_count() or 1
-    aff, quota = allowed_cpus()
-    # every allowed core: the affinity mask, bounded by the cgroup quota (the
-    # GPU box's share per GPU; 16 if a whole machine is visible and no quota
-    # says otherwise)
-    workers = aff if quota is None else min(aff, max(1, int(quota)))
-    if quota is None and aff > 64:
-        workers = 16
+    workers, aff, quota = cpu_workers()
     full = _cpu_inputs(full_bins, dmax, seed) if full_bins else None
     sample = _cpu_inputs(sample_bins, dmax, seed)
     ctx = multiprocessing.get_context('fork')
@@ -334,6 +433,100 @@ def cpu_baseline_run(full_bins, sample_bins, dmax, seed=123, full_runs=1):
     return base, {'raw': sample['raw'], 'f': sample['f'],
                   'dist': sample['dist'], 'design': sample['design'],
                   'p_fixed': p_fixed, 'p_faithful': p_faith}
+
+
+def cpu_workers():
+    """Every allowed core: the affinity mask bounded by the cgroup quota (the
+    GPU box's share per GPU; 16 if a whole machine is visible and no quota
+    says otherwise). Returns (workers, affinity, quota)."""
+    aff, quota = allowed_cpus()
+    workers = aff if quota is None else min(aff, max(1, int(quota)))
+    if quota is None and aff > 64:
+        workers = 16
+    return workers, aff, quota
+
+
+def cfg3_genome(dmax):
+    """The cfg3 genome (BASELINE configs[2]) as other_config('cfg3') draws
+    it: 20 mm10-sized chromosomes, seed 0, concatenated."""
+    from hic3defdr_amd import synthetic
+    t0 = time.perf_counter()
+    parts = synthetic.draw_genome(list(synthetic.MM10_BINS), (2, 2), dmax,
+                                  seed=0, workers=16)
+    g = {'raw': np.concatenate([p[0] for p in parts]),
+         'f': np.concatenate([p[1] for p in parts]),
+         'dist': np.concatenate([p[2] for p in parts])}
+    del parts
+    g['generate_s'] = time.perf_counter() - t0
+    return g
+
+
+def cpu_cfg3_run(genome, dmax):
+    """The north star's headline CPU leg: the fallback-fixed restatement's
+    estimate_disp + lrt ONCE over the whole cfg3 genome (every distance pooled
+    genome-wide, as analysis.py:169-206) on every allowed core. Returns (the
+    row, p, disp_per_dist)."""
+    import multiprocessing
+    workers, aff, quota = cpu_workers()
+    design = np.zeros((4, 2), dtype=bool)
+    design[[0, 1], 0] = design[[2, 3], 1] = True
+    ctx = multiprocessing.get_context('fork')
+    with ctx.Pool(workers) as pool:
+        t0 = time.perf_counter()
+        p, dpd = cpu_pipeline(pool, workers, genome['raw'], genome['f'],
+                              genome['dist'], design, dmax + 1, False,
+                              with_table=True, progress=True)
+        el = time.perf_counter() - t0
+    n = len(genome['raw'])
+    row = {'value': n / el, 'unit': 'pixels/s', 'cores': workers,
+           'affinity_cpus': aff, 'cgroup_quota_cpus': quota, 'kind': 'port',
+           'variant': 'fallback-fixed restatement (oracle/), qcml per '
+                      '(distance, condition) on the pool, LRT over pixel '
+                      'blocks on the pool',
+           'elapsed_s': el,
+           'sample': 'the WHOLE cfg3 genome, one run: 20 mm10-sized '
+                     'chromosomes, %d disp pixels, dmax %d' % (n, dmax),
+           'calibration_vs_reference': cpu_calibration()}
+    return row, p, dpd
+
+
+def cfg3_vs_cpu(ctx, p, dpd, cpu_p, cpu_dpd, dmax):
+    """The GPU's cfg3 result against the CPU restatement's on the same
+    genome: p per pixel, the genome-wide BH calls at three FDRs, and the
+    segments whose disp_per_dist differs beyond 1e-6 (with the move in delta
+    = disp / (1 + disp) in units of Brent's xatol 1e-5, dispersion.py:46-80:
+    near-tied NLL comparisons)."""
+    import oracle
+    with np.errstate(all='ignore'):
+        rel = np.abs(p - cpu_p) / np.maximum(cpu_p, 1e-300)
+    rel[p == cpu_p] = 0.0
+    q = ctx.bh(p)
+    cq = oracle.adjust_pvalues(cpu_p)
+    calls = {}
+    for fdr in (0.01, 0.05, 0.1):
+        a, b = q < fdr, cq < fdr
+        calls['%g' % fdr] = {'gpu': int(a.sum()), 'cpu': int(b.sum()),
+                             'differ': int(np.sum(a != b))}
+    fin = np.isfinite(cpu_dpd)
+    drel = np.zeros_like(cpu_dpd)
+    drel[fin] = np.abs(dpd[fin] - cpu_dpd[fin]) / np.abs(cpu_dpd[fin])
+    segs = [{'distance': int(d), 'condition': int(c),
+             'rel': float(drel[d, c]),
+             'd_delta_over_xatol': float(abs(
+                 dpd[d, c] / (1 + dpd[d, c])
+                 - cpu_dpd[d, c] / (1 + cpu_dpd[d, c])) / 1e-5)}
+            for d, c in zip(*np.nonzero(drel > 1e-6))]
+    return {'pixels': int(len(p)),
+            'max_rel_dp': float(rel.max()),
+            'pixels_rel_dp_gt_1e-6': int(np.sum(rel > 1e-6)),
+            'max_abs_dq': float(np.max(np.abs(q - cq))),
+            'calls': calls,
+            'identical_calls': all(v['differ'] == 0 for v in calls.values()),
+            'disp_per_dist_max_rel': float(drel.max()),
+            'segments_beyond_1e-6': segs,
+            'note': 'GPU (product kernels, device BH) vs the CPU restatement '
+                    '(oracle/, BH = lib5c adjust_pvalues restated) on the same '
+                    'genome; q-value calls at FDR 0.01 / 0.05 / 0.1'}
 
 
 def sample_parity(ctx, sample, dmax):
@@ -439,6 +632,52 @@ def make_workload(tmp, name, bins, dmax, seed):
     return h, kw
 
 
+def e2e_cfg3_files(dmax):
+    """The cfg3 genome written in the reference's input layout (per-replicate
+    NPZ + bias files, loop clusters; synthetic.write_genome, a process pool)
+    -- before the GPU is touched. Returns (directory, constructor kwargs,
+    seconds)."""
+    from hic3defdr_amd import synthetic
+    base = tempfile.mkdtemp(prefix='h3dbench_cfg3e2e_')
+    t0 = time.perf_counter()
+    kw = synthetic.write_genome(base, synthetic.MM10_BINS, seed=3, workers=16,
+                                dmax=dmax)
+    return base, kw, time.perf_counter() - t0
+
+
+def e2e_cfg3(base, kw, write_s, runs=2):
+    """BASELINE configs[2] end to end through the class on one GPU: the 20
+    chromosomes from their files through HiC3DeFDR.run_to_qvalues()'s stages
+    (analysis.py:305-364: prepare_data per chromosome, the genome-wide
+    estimate_disp, lrt, the loop-pixel BH), per stage, after one run paying
+    the first-call costs (reported apart)."""
+    import pandas as pd
+    from hic3defdr_amd import HiC3DeFDR
+
+    class _H:                     # the constructor arguments, no outdir yet
+        pass
+    h = _H()
+    h.raw_npz_patterns, h.bias_patterns = kw['raw_npz_patterns'], \
+        kw['bias_patterns']
+    h.chroms = kw['chroms']
+    h.design = pd.DataFrame(kw['design'], index=kw['reps'],
+                            columns=kw['conds'])
+    h.dist_thresh_max, h.loop_patterns, h.res = 200, kw['loop_patterns'], \
+        10000
+    first = _e2e_once(h, base, 'first', drop=True)
+    per = [_e2e_once(h, base, k, drop=True) for k in range(runs)]
+    out = {k: statistics.median(r[k] for r in per) for k in per[0]
+           if k != 'note'}
+    out['runs_total_s'] = [r['total_s'] for r in per]
+    out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
+    out['write_genome_s'] = write_s
+    out['chromosomes'] = len(kw['chroms'])
+    out['note'] = ('cfg3 from files: 20 mm10-sized chromosomes (seed 3), 4 '
+                   'reps, dmax 200, loop clusters; ' + per[0]['note'] +
+                   '; per-stage medians of %d runs after the first' % runs)
+    return out
+
+
 def e2e_wall(h, tmp, runs=3):
     """The product's whole run_to_qvalues on the same workload files (host
     I/O included), per stage: each stage's median over ``runs`` runs (a new
@@ -456,14 +695,15 @@ def e2e_wall(h, tmp, runs=3):
     return out
 
 
-def _e2e_once(h, tmp, k):
+def _e2e_once(h, tmp, k, drop=False):
     from hic3defdr_amd import HiC3DeFDR
-    out = os.path.join(tmp, 'out_e2e_%d' % k)
+    out = os.path.join(tmp, 'out_e2e_%s' % k)
     os.makedirs(out, exist_ok=True)
     h2 = HiC3DeFDR(raw_npz_patterns=h.raw_npz_patterns,
                    bias_patterns=h.bias_patterns, chroms=h.chroms,
                    design=h.design, outdir=out,
-                   dist_thresh_max=h.dist_thresh_max)
+                   dist_thresh_max=h.dist_thresh_max,
+                   loop_patterns=h.loop_patterns, res=h.res)
     t = [time.perf_counter()]
     h2.prepare_data(verbose=False)
     t.append(time.perf_counter())
@@ -475,6 +715,9 @@ def _e2e_once(h, tmp, k):
     t.append(time.perf_counter())
     h2.flush()
     t.append(time.perf_counter())
+    del h2
+    if drop:
+        shutil.rmtree(out, ignore_errors=True)
     return {'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
             'estimate_disp_s': t[2] - t[1], 'lrt_s': t[3] - t[2],
             'bh_s': t[4] - t[3], 'outdir_flush_s': t[5] - t[4],
@@ -600,7 +843,7 @@ def total_over_ranks(dist, dev, n):
 
 
 def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
-               dmax, workload, parallelism, scaling):
+               dmax, workload, parallelism, scaling, peaks=None):
     w_ms, w_n, w_bytes = ev['disp_work']
     l_ms, l_n, _ = ev['lrt']
     n_ms, n_n, n_bytes = per['disp_nll']
@@ -624,13 +867,29 @@ def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
     # the table-fed instantiation the resident distance path launches
     lrt_pmc = pmc_kernel('k_lrt<4, 2, true>', bins, dmax) \
         or pmc_kernel('k_lrt<4, 2, false>', bins, dmax)
-    eq_fp64 = fp64_roof(eq_pmc, w_avg_s)
+    pk_fp64, pk_hbm = _peak(peaks, 'fp64'), _peak(peaks, 'hbm')
+    eq_fp64 = fp64_roof(eq_pmc, w_avg_s, pk_fp64)
+    # the same kernel's launch time from the committed rocprofv3 stats of
+    # this command (another run, often another box): the fraction the
+    # committed profiles reproduce
+    eq_rp = rocprof_avg_us('k_disp_work<2, 4, 0, false>', bins, dmax)
+    eq_fp64_rp = fp64_roof(eq_pmc, eq_rp['avg_us'] / 1e6, pk_fp64) \
+        if eq_rp else None
     roof = {
         'bound': 'fp64', 'kernel': 'k_disp_work<2,4,kEqualize,false> (equalize pass)',
         'achieved': eq_fp64['achieved'] if eq_fp64 else None,
         'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
         'frac': eq_fp64['frac'] if eq_fp64 else None,
         'useful_frac': eq_fp64.get('useful_frac') if eq_fp64 else None,
+        'peak_measured': pk_fp64,
+        'frac_measured': eq_fp64.get('frac_measured') if eq_fp64 else None,
+        'peak_source': 'peak: AMD MI355X spec, vector FP64 dense; '
+                       'peak_measured: this GPU, measured_peaks (FMA chains)',
+        'rocprof': {'avg_launch_us': eq_rp['avg_us'], 'calls': eq_rp['calls'],
+                    'frac': eq_fp64_rp['frac'],
+                    'frac_measured': eq_fp64_rp.get('frac_measured'),
+                    'source': eq_rp['source'], 'command': eq_rp['command']}
+        if eq_fp64_rp else None,
         'lane_util': eq_pmc['lane_util'] if eq_pmc else None,
         'flops_per_launch': eq_pmc['f64_flops'] if eq_pmc else None,
         'flops_source': 'FP64 flops issued per launch, PMC '
@@ -643,6 +902,8 @@ def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
         'avg_launch_us': w_avg_s * 1e6, 'launches': w_n,
         'hbm': {'achieved': w_ach, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': w_ach / HBM_PEAK_GBS,
+                'peak_measured': pk_hbm,
+                'frac_measured': w_ach / pk_hbm if pk_hbm else None,
                 'bytes_per_launch': w_bpl,
                 'note': 'algorithmic: 20 B per equalize pixel-'
                         'replicate (raw 4 + f 8 in, pseudodata 8 '
@@ -664,7 +925,7 @@ def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
         'roofline': roof,
         'kernel_rooflines': {
             'nll_brent': {
-                'fp64': fp64_roof(nll_pmc, n_avg_s),
+                'fp64': fp64_roof(nll_pmc, n_avg_s, pk_fp64),
                 'hbm_traffic_per_launch': nll_pmc['hbm_bytes']
                 if nll_pmc else None,
                 'algorithmic_bytes_per_launch': n_bytes / n_iter,
@@ -672,14 +933,18 @@ def bench_line(args, world, n_local, tot_px, R, C, elapsed, ev, per, bins,
                 'note': 'per qcml iteration: k_brent + k_brent_gang (both '
                         'launched, the device runs one), PMC summed over '
                         'both'},
-            'lrt': {'fp64': fp64_roof(lrt_pmc, l_avg_s),
+            'lrt': {'fp64': fp64_roof(lrt_pmc, l_avg_s, pk_fp64),
                     'hbm': {'achieved': l_ach, 'peak': HBM_PEAK_GBS,
                             'unit': 'GB/s', 'frac': l_ach / HBM_PEAK_GBS,
+                            'peak_measured': pk_hbm,
+                            'frac_measured': l_ach / pk_hbm if pk_hbm
+                            else None,
                             'bytes_per_pixel': bytes_per_lrt_pixel(R, C)},
                     'hbm_traffic_per_launch': lrt_pmc['hbm_bytes']
                     if lrt_pmc else None,
                     'avg_launch_us': l_avg_s * 1e6}},
         'kernels_ms_per_step': kernels,
+        'measured_peaks': peaks,
         'work_per_step': {
             'equalize_pixel_reps': w_bytes / 20.0 / args.steps,
             'nll_pixel_reps': n_bytes / 8.0,
@@ -701,26 +966,33 @@ OTHER_CONFIGS = {
 }
 
 
-def other_config(torch, ctx, dev, name, steps=2, warmup=1):
+def other_config(torch, ctx, dev, name, steps=2, warmup=1, genome=None,
+                 keep=None):
     """One of the other north-star shapes through the bench's step
     (estimate_disp + tables + lrt on HBM-resident inputs, as cfg2), timed on
     this GPU after the headline measurement: `steps` steps after `warmup`,
-    kernel times from one extra profiled step."""
+    kernel times from one extra profiled step. ``genome``: the inputs already
+    drawn (cfg3_genome); ``keep`` (a dict): receives the last step's p and
+    disp_per_dist."""
     from hic3defdr_amd import synthetic
     cfg = OTHER_CONFIGS[name]
     bins = list(synthetic.MM10_BINS) if name == 'cfg3' else [49792]
     t0 = time.perf_counter()
-    # (one chromosome: its replicates on the threads; the data do not depend
-    # on the thread count -- a seeded stream per replicate)
-    parts = synthetic.draw_genome(bins, cfg['npc'], cfg['dmax'], seed=0,
-                                  workers=16) if len(bins) > 1 else \
-        [synthetic.draw_band(bins[0], cfg['npc'], cfg['dmax'], seed=0,
-                             chrom_index=0, workers=16)]
-    raw = np.concatenate([p[0] for p in parts])
-    f = np.concatenate([p[1] for p in parts])
-    dist_np = np.concatenate([p[2] for p in parts])
-    del parts
-    gen_s = time.perf_counter() - t0
+    if genome is not None:
+        raw, f, dist_np = genome['raw'], genome['f'], genome['dist']
+        gen_s = genome['generate_s']
+    else:
+        # (one chromosome: its replicates on the threads; the data do not
+        # depend on the thread count -- a seeded stream per replicate)
+        parts = synthetic.draw_genome(bins, cfg['npc'], cfg['dmax'], seed=0,
+                                      workers=16) if len(bins) > 1 else \
+            [synthetic.draw_band(bins[0], cfg['npc'], cfg['dmax'], seed=0,
+                                 chrom_index=0, workers=16)]
+        raw = np.concatenate([p[0] for p in parts])
+        f = np.concatenate([p[1] for p in parts])
+        dist_np = np.concatenate([p[2] for p in parts])
+        del parts
+        gen_s = time.perf_counter() - t0
     n, R = raw.shape
     C = len(cfg['npc'])
     D = cfg['dmax'] + 1
@@ -728,6 +1000,7 @@ def other_config(torch, ctx, dev, name, steps=2, warmup=1):
     t_raw, t_f, t_dist = _upload(torch, dev, raw, f, dist_np)
     present = np.isin(np.arange(D), dist_np)
     del raw, f, dist_np
+    genome = None
     o = _outputs(torch, dev, n, C)
     torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)
@@ -757,8 +1030,12 @@ def other_config(torch, ctx, dev, name, steps=2, warmup=1):
     ks = {k: ctx.profile_read(k)[0] for k in
           ('disp_work', 'disp_nll', 'disp_update', 'disp_prep', 'lrt')}
     p = o['p'].cpu().numpy()
+    if keep is not None:
+        keep['p'], keep['dpd'] = p, dpd
     ctx.set_stream(None)
     torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    del o, t_raw, t_f, t_dist
+    torch.cuda.empty_cache()
     return {
         'workload': cfg['workload'], 'bins': int(sum(bins)), 'reps': int(R),
         'conds': int(C), 'disp_pixels': int(n), 'steps': steps,
@@ -774,7 +1051,8 @@ def other_config(torch, ctx, dev, name, steps=2, warmup=1):
                 np.array_equal(first, dpd, equal_nan=True))}}
 
 
-def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
+def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
+             peaks=None):
     """Weak scaling: one 20k-bin chromosome per rank (BASELINE configs[1])."""
     import torch
     from hic3defdr_amd import _native, parallel
@@ -841,7 +1119,8 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
                 'in-kernel Brent searches' if world == 1 else
                 'distance re-shard: all_to_all of the disp pixels, in-kernel '
                 'Brent per rank, table all-reduce' if by_dist
-                else 'per-pass NLL all-reduce over RCCL'), 'weak')
+                else 'per-pass NLL all-reduce over RCCL'), 'weak',
+            peaks=peaks)
         out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
         if world == 1:
             out['parity_vs_reference'] = parity_vs_reference(
@@ -851,16 +1130,36 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu):
             out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
         if world == 1 and not args.no_e2e:
             out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
+            if cfg3 and cfg3.get('files'):
+                base, kw, w_s = cfg3['files']
+                try:
+                    out['e2e_cfg3_run_to_qvalues'] = e2e_cfg3(base, kw, w_s)
+                finally:
+                    shutil.rmtree(base, ignore_errors=True)
         if world == 1 and not args.no_other_configs:
-            out['other_configs'] = {
-                name: other_config(torch, ctx, dev, name)
-                for name in ('cfg3', 'cfg4')}
+            oc, keep = {}, {}
+            g3 = cfg3.pop('genome', None) if cfg3 else None
+            oc['cfg3'] = other_config(torch, ctx, dev, 'cfg3', genome=g3,
+                                      keep=keep)
+            del g3
+            if cfg3 and 'cpu' in cfg3:
+                row, cpu_p, cpu_dpd = cfg3.pop('cpu')
+                row['gpu_over_cpu'] = oc['cfg3']['value'] / row['value']
+                oc['cfg3']['cpu_baseline'] = row
+                par = cfg3_vs_cpu(ctx, keep['p'], keep['dpd'], cpu_p, cpu_dpd,
+                                  OTHER_CONFIGS['cfg3']['dmax'])
+                oc['cfg3']['vs_cpu_restatement'] = par
+                oc['cfg3']['identical_calls'] = par['identical_calls']
+                del cpu_p, cpu_dpd
+            keep.clear()
+            oc['cfg4'] = other_config(torch, ctx, dev, 'cfg4')
+            out['other_configs'] = oc
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def run_cfg3(args, world, rank, local, dist, ctx, dev):
+def run_cfg3(args, world, rank, local, dist, ctx, dev, peaks=None):
     """Strong scaling over the whole mouse genome (BASELINE configs[2])."""
     import torch
     from hic3defdr_amd import _native, parallel, synthetic
@@ -972,7 +1271,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev):
                       'the disp pixels, single-GPU driver per rank, table '
                       'all-reduce), LRT on own chromosomes, genome-wide BH '
                       'as a sample sort over the ranks (two all_to_alls of '
-                      'the p-values)'), 'strong')
+                      'the p-values)'), 'strong', peaks=peaks)
     out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
     out['config']['chromosomes_rank0'] = [int(i) for i in mine]
     out['config']['generate_s_rank0'] = gen_s
@@ -1008,6 +1307,12 @@ def main():
                     help='runs of the full-chromosome CPU row (median)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-e2e', action='store_true')
+    ap.add_argument('--no-e2e-cfg3', action='store_true',
+                    help='skip the cfg3 run_to_qvalues-from-files leg')
+    ap.add_argument('--no-cpu-cfg3', action='store_true',
+                    help='skip the whole-genome CPU restatement run (cfg3)')
+    ap.add_argument('--no-peaks', action='store_true',
+                    help='skip the measured FP64 / HBM peaks')
     ap.add_argument('--no-other-configs', action='store_true',
                     help='skip the cfg3 / cfg4 lines measured after the '
                          'headline (N = 1)')
@@ -1027,13 +1332,27 @@ def main():
     backend = os.environ.get('H3D_BENCH_BACKEND', 'nccl')
     config = args.config if args.config != 'auto' else \
         ('cfg2' if world == 1 else 'cfg3')
-    cpu = None
+    cpu, cfg3 = None, {}
     if world == 1 and config == 'cfg2' and not args.no_cpu_baseline:
         cpu = cpu_baseline_run(args.cpu_full_bins, args.cpu_bins,
                                args.dmax, full_runs=args.cpu_full_runs)
         # (before the GPU: the pool forks)
+    if world == 1 and config == 'cfg2':
+        d3 = OTHER_CONFIGS['cfg3']['dmax']
+        if not args.no_other_configs:
+            cfg3['genome'] = cfg3_genome(d3)
+            if not args.no_cpu_baseline and not args.no_cpu_cfg3:
+                print('bench: cfg3 CPU leg (whole genome, %d pixels) ...'
+                      % len(cfg3['genome']['raw']), file=sys.stderr,
+                      flush=True)
+                cfg3['cpu'] = cpu_cfg3_run(cfg3['genome'], d3)
+        if not args.no_e2e and not args.no_e2e_cfg3:
+            cfg3['files'] = e2e_cfg3_files(d3)
     import torch
     torch.cuda.set_device(local)
+    peaks = None
+    if rank == 0 and not args.no_peaks:
+        peaks = measured_peaks(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -1047,9 +1366,10 @@ def main():
     dev = torch.device('cuda', local)
     try:
         if config == 'cfg2':
-            out = run_cfg2(args, world, rank, local, dist, ctx, dev, cpu)
+            out = run_cfg2(args, world, rank, local, dist, ctx, dev, cpu,
+                           cfg3, peaks)
         else:
-            out = run_cfg3(args, world, rank, local, dist, ctx, dev)
+            out = run_cfg3(args, world, rank, local, dist, ctx, dev, peaks)
         if rank == 0:
             print(json.dumps(out), flush=True)
     finally:

@@ -8,6 +8,9 @@
                           by CPU unit tests (tests/test_special_host.py).
 - ``libh3d_selftest.so`` the same numerics compiled for gfx950 behind the same
                           test ABI, used only by GPU unit tests.
+- ``libh3d_peak.so``     bench.py's measured roofline denominators (an FP64
+                          FMA-chain kernel and a 16 B/lane copy); measurement
+                          only, never loaded by the product.
 
 All land in ``hic3defdr_amd/lib/`` so they travel to the GPU box with the
 repo snapshot (they are git-ignored, not gpurun-ignored).
@@ -100,6 +103,14 @@ def build_selftest(force=False):
     return _build(out, cmd, [src] + _headers(), force)
 
 
+def build_peak(force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, 'libh3d_peak.so')
+    src = os.path.join(CSRC, 'h3d_peak.hip')
+    cmd = [HIPCC] + HIP_FLAGS + ['-shared', '-o', out, src]
+    return _build(out, cmd, [src], force)
+
+
 def _native_objects(objdir=None, extra=()):
     """(object, compile command, deps) of every TU of libh3d.so."""
     hdrs = _headers()
@@ -164,7 +175,8 @@ def build_all(force=False):
         futs = [ex.submit(_build, o, c, d, force)
                 for o, c, d in _native_objects()]
         futs += [ex.submit(build_hosttest, force),
-                 ex.submit(build_selftest, force)]
+                 ex.submit(build_selftest, force),
+                 ex.submit(build_peak, force)]
         for f in futs:
             f.result()
     return (_link_native(force), os.path.join(LIBDIR, 'libh3d_hosttest.so'),

@@ -13,7 +13,17 @@ test_gpu_scale.py (the full cfg2 chromosome) and the fixture-size goldens:
 - the genome-wide BH is the CPU oracle's BH on the same p, bit for bit, and
   q is monotone in p;
 - a second run is bit-identical (deterministic reductions at 46 M pixels:
-  the 2^31-element scratch caps, the segment sums over 20 chromosomes).
+  the 2^31-element scratch caps, the segment sums over 20 chromosomes);
+- six whole genome-wide segments (distances 4, 100, 200 in both conditions,
+  each pooling ~160-260 k pixels of 20 chromosomes): the CPU oracle's qcml
+  (dispersion.py:10-43, pinned to the reference's goldens) vs the GPU's
+  disp_per_dist at 1e-6, at most one near-tied Brent comparison (within
+  xatol in delta) as test_gpu_scale.py;
+- 3,000 sampled pixels: the oracle's lrt (lrt.py:7-50) with the GPU's own
+  tables vs the GPU's p and llr at 1e-6 relative.
+The same comparison over every pixel of the genome -- the CPU restatement's
+whole estimate_disp + lrt + BH against the GPU's, calls at three FDRs -- is
+bench.py's other_configs.cfg3.vs_cpu_restatement.
 """
 import numpy as np
 import pytest
@@ -34,22 +44,34 @@ def cfg3():
     return raw, f, dist
 
 
-def test_cfg3_whole_genome(cfg3):
-    import oracle
+COND = np.array([0, 0, 1, 1], dtype=np.int32)
+
+
+@pytest.fixture(scope='module')
+def cfg3_runs(cfg3):
+    """Two GPU runs of the genome: (disp_per_dist, tables, p, llr, mu0,
+    mu1, q) each."""
     from hic3defdr_amd import _native
     ctx = _native.context(0)
     raw, f, dist = cfg3
-    assert len(raw) > 40_000_000
-    cond = np.array([0, 0, 1, 1], dtype=np.int32)
     C, D = 2, DMAX + 1
     runs = []
     for _ in range(2):
-        dpd = ctx.disp_per_dist(raw, f, dist, cond, C, D)  # raises on flags
+        dpd = ctx.disp_per_dist(raw, f, dist, COND, C, D)  # raises on flags
         tab = _native.disp_tables(dpd)
-        p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, cond, want_disp=False)
+        p, llr, m0, m1, _ = ctx.lrt(raw, f, dist, tab, COND, want_disp=False)
         q = ctx.bh(p)
-        runs.append((dpd, p, llr, m0, m1, q))
-    dpd, p, llr, m0, m1, q = runs[0]
+        runs.append((dpd, tab, p, llr, m0, m1, q))
+    return runs
+
+
+def test_cfg3_whole_genome(cfg3, cfg3_runs):
+    import oracle
+    raw, f, dist = cfg3
+    assert len(raw) > 40_000_000
+    C, D = 2, DMAX + 1
+    runs = cfg3_runs
+    dpd, _, p, llr, m0, m1, q = runs[0]
     present = np.isin(np.arange(D), dist)
     assert present[4:].all() and not present[:4].any()
     assert np.all(np.isfinite(dpd[present]))
@@ -65,6 +87,51 @@ def test_cfg3_whole_genome(cfg3):
     assert np.all(np.diff(q[o]) >= 0) and np.all(q >= p) and np.all(q <= 1)
     for a, b in zip(runs[0], runs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_cfg3_segments_vs_oracle(cfg3, cfg3_runs):
+    """Whole genome-wide segments (every chromosome's pixels at one distance,
+    one condition) through the oracle's qcml vs the GPU's disp_per_dist."""
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    raw, f, dist = cfg3
+    dpd = cfg3_runs[0][0]
+    jobs, keys = [], []
+    for d in (4, 100, 200):
+        sel = np.flatnonzero(dist == d)
+        for c in range(2):
+            reps = COND == c
+            jobs.append((raw[sel][:, reps].astype(float), f[sel][:, reps]))
+            keys.append((d, c))
+    # (numpy / scipy release the GIL: ~10 s for the six on the host)
+    with ThreadPoolExecutor(6) as ex:
+        want = np.array(list(ex.map(lambda a: oracle.qcml(*a), jobs)))
+    got = np.array([dpd[d, c] for d, c in keys])
+    rel = np.abs(got - want) / np.abs(want)
+    ddelta = np.abs(got / (1 + got) - want / (1 + want))
+    print('cfg3 segments vs the oracle: %s rel %s, |d delta| %s' % (
+        keys, np.array2string(rel, precision=2),
+        np.array2string(ddelta, precision=2)))
+    # a near-tied Brent comparison can send one search to another point
+    # inside its tolerance (xatol 1e-5 in delta; test_gpu_scale.py)
+    assert np.sum(rel > 1e-6) <= 1, rel
+    assert np.all(ddelta <= 1e-5), ddelta
+
+
+def test_cfg3_lrt_sample_vs_oracle(cfg3, cfg3_runs):
+    """3,000 pixels sampled over the genome through the oracle's lrt with
+    the GPU's own tables (lrt.py:7-50) vs the GPU's p and llr."""
+    import oracle
+    raw, f, dist = cfg3
+    _, tab, p, llr, _, _, _ = cfg3_runs[0]
+    rng = np.random.default_rng(1)
+    idx = np.sort(rng.choice(len(raw), 3000, replace=False))
+    design = np.zeros((4, 2), dtype=bool)
+    design[np.arange(4), COND] = True
+    disp = tab[dist[idx]][:, COND]          # lrt.py's per-replicate disp
+    p_o, llr_o, _, _ = oracle.lrt(raw[idx].astype(float), f[idx], disp, design)
+    np.testing.assert_allclose(p[idx], p_o, rtol=1e-6, atol=1e-300)
+    np.testing.assert_allclose(llr[idx], llr_o, rtol=1e-6, atol=1e-9)
 
 
 def test_cfg3_through_the_class():
