@@ -305,6 +305,10 @@ class AnalyzingHiC3DeFDR(object):
         t_raw, t_f, t_dist, offsets = res.disp_pixels(sh.mine, R)
         n = int(t_raw.shape[0])
         t_tab = torch.empty((D, C), dtype=torch.float64, device=res.dev)
+        t_disp = torch.empty((n, C), dtype=torch.float64, device=res.dev)
+        # lrt's outputs, allocated before the disp copy below starts paging in
+        # its host array (resident.lrt_buffers)
+        lrt_bufs = res.lrt_buffers(n, C)
         if sh.sharded:
             disp_per_dist = self._disp_per_dist_sharded(t_raw, t_f, t_dist, C,
                                                         D)
@@ -322,7 +326,6 @@ class AnalyzingHiC3DeFDR(object):
                 t_tab.data_ptr(), weighted=weighted_lowess, frac=frac,
                 auto_frac_factor=auto_frac_factor)
         eprint('  fitting distance vs dispersion relationship')
-        t_disp = torch.empty((n, C), dtype=torch.float64, device=res.dev)
         # settles the device smoother (a degenerate fit is redone on the host)
         ctx.table_gather_dev(t_tab.data_ptr(), D, C,
                              t_dist.data_ptr() if n else None, n,
@@ -345,7 +348,8 @@ class AnalyzingHiC3DeFDR(object):
                            ready=disp_ready)
         if sh.rank == 0:
             self.save_data(disp_per_dist, 'disp_per_dist')
-        res.start_session(sh.mine, t_raw, t_f, t_dist, offsets, t_tab, D, C)
+        res.start_session(sh.mine, t_raw, t_f, t_dist, offsets, t_tab, D, C,
+                          lrt_bufs)
         self._barrier(sh)
 
     def _estimate_disp_callable(self, estimator, frac, auto_frac_factor,
@@ -392,8 +396,12 @@ class AnalyzingHiC3DeFDR(object):
         if sess is not None:
             for c in chroms:
                 eprint('running LRT for chrom %s' % c, skip=not verbose)
+            # the session's preallocated outputs serve its first lrt only
+            # (the host arrays then belong to the outdir queue)
+            bufs, sess['bufs'] = sess.get('bufs'), None
             self._lrt_run(res, chroms, sess['raw'], sess['f'], sess['dist'],
-                          sess['offsets'], refit_mu, table=sess['tables'])
+                          sess['offsets'], refit_mu, table=sess['tables'],
+                          bufs=bufs)
         else:
             for c in chroms:
                 eprint('running LRT for chrom %s' % c, skip=not verbose)
@@ -406,18 +414,21 @@ class AnalyzingHiC3DeFDR(object):
             self._barrier(sh)
 
     def _lrt_run(self, res, chroms, t_raw, t_f, t_dist, offsets, refit_mu,
-                 table=None, disp=None):
+                 table=None, disp=None, bufs=None):
         """One LRT launch over the concatenated disp pixels of ``chroms``:
         with the device ``table`` (D, C) and t_dist, or the per-pixel
         ``disp`` (n, C) from the outdir; the four outputs saved per
-        chromosome (write-behind)."""
+        chromosome (write-behind). ``bufs``: preallocated outputs
+        (Resident.lrt_buffers)."""
         import torch
         ctx = self._ctx()
         n = int(t_raw.shape[0])
         C = self.design.shape[1]
+        if n and (bufs is None or bufs[0].shape[1] != n
+                  or bufs[1].shape[1] != C):
+            bufs = res.lrt_buffers(n, C)
         if n:
-            tp = torch.empty((3, n), dtype=torch.float64, device=res.dev)
-            t1 = torch.empty((n, C), dtype=torch.float64, device=res.dev)
+            tp, t1, h3_dst, h1_dst = bufs
             ptrs = (tp[0].data_ptr(), tp[1].data_ptr(), tp[2].data_ptr(),
                     t1.data_ptr())
             if table is not None:
@@ -432,8 +443,8 @@ class AnalyzingHiC3DeFDR(object):
             # (the lrt calls return with the ctx stream drained); the outputs
             # reach the outdir by background copies (analysis/d2h.py), waited
             # for by their writer / first reader
-            h3, r3 = to_host_async(tp)
-            mu1, r1 = to_host_async(t1)
+            h3, r3 = to_host_async(tp, dst=h3_dst)
+            mu1, r1 = to_host_async(t1, dst=h1_dst)
         else:
             tp = None
             h3, mu1 = np.empty((3, 0)), np.empty((0, C))

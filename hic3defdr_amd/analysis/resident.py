@@ -252,17 +252,31 @@ class Resident(object):
                 t_dist.data_ptr() + o * 4 if e.n_disp else None)
         return t_raw, t_f, t_dist, offsets
 
-    def start_session(self, chroms, t_raw, t_f, t_dist, offsets, t_tab, D, C):
+    def lrt_buffers(self, n, C):
+        """The LRT's outputs for ``n`` pixels, device and host: (p / llr /
+        mu0 as one (3, n) tensor, mu1 (n, C); their host destinations).
+        estimate_disp allocates them before its own results start streaming
+        to the host (analysis/d2h.py: a large host allocation waits for the
+        copy thread's page faults), the session hands them to lrt once."""
+        torch = self.torch
+        if not n:
+            return None
+        return (torch.empty((3, n), dtype=torch.float64, device=self.dev),
+                torch.empty((n, C), dtype=torch.float64, device=self.dev),
+                np.empty((3, n)), np.empty((n, C)))
+
+    def start_session(self, chroms, t_raw, t_f, t_dist, offsets, t_tab, D, C,
+                      lrt_bufs=None):
         """estimate_disp's resident result for lrt: its pixels and device
         tables, valid while its disp files and its chromosomes' stage files
-        are current."""
+        are current; ``lrt_bufs`` (lrt_buffers) for the first lrt on it."""
         files = {}
         for c in chroms:
             files[self.h._npy('disp', c)] = self._token(self.h._npy('disp', c))
             files.update(self.chroms[c].files)
         self.session = {'chroms': tuple(chroms), 'raw': t_raw, 'f': t_f,
                         'dist': t_dist, 'offsets': offsets, 'tables': t_tab,
-                        'D': D, 'C': C, 'files': files}
+                        'D': D, 'C': C, 'files': files, 'bufs': lrt_bufs}
 
     def keep_pvalues(self, chroms, t_p, offsets):
         """lrt's device p-values of ``chroms`` (its pvalues files just

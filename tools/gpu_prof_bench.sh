@@ -6,7 +6,7 @@ tag=${1:-prof}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-  -d gpurun_out/${tag}_prof -o run -- python3 -u bench.py --no-cpu-baseline --no-e2e --no-other-configs \
+  -d gpurun_out/${tag}_prof -o run -- python3 -u bench.py --no-cpu-baseline --no-e2e --no-other-configs --no-peaks \
   > gpurun_out/${tag}_prof_bench.json 2> gpurun_out/${tag}_prof.err
 python3 - "$tag" <<'PY'
 import csv, glob, sys
