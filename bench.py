@@ -1175,8 +1175,23 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev, peaks=None):
     assign = parallel.lpt_assign({i: b for i, b in enumerate(bins)}, e_world)
     mine = sorted(assign[e_rank])
     t0 = time.perf_counter()
+    # the re-shard ships the keys of f (row, chromosome, size-factor row;
+    # H3D_RESHARD_FULL=1: the full record with f)
+    compact = world > 1 and os.environ.get('H3D_RESHARD_FULL') != '1'
     parts = synthetic.draw_genome(bins, (2, 2), dmax, seed=0,
-                                  indices=None if emu else mine, workers=16)
+                                  indices=None if emu else mine, workers=16,
+                                  keys=compact)
+    keys = None
+    if compact:
+        keys = parallel.PixelKeys(
+            torch.from_numpy(np.concatenate([p[3] for p in parts])).to(dev),
+            torch.from_numpy(np.concatenate(
+                [np.full(len(p[0]), i, dtype=np.int32)
+                 for i, p in zip(mine, parts)])).to(dev),
+            torch.zeros(sum(len(p[0]) for p in parts), dtype=torch.int32,
+                        device=dev),
+            {i: (p[4], np.ones((1, 4))) for i, p in zip(mine, parts)},
+            len(bins))
     if emu:
         own = [p for i, p in enumerate(parts) if i in mine]
         d_all = np.concatenate([p[2] for p in parts])
@@ -1227,7 +1242,7 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev, peaks=None):
                                         reduce=reduce)
         elif world > 1:
             dpd = parallel.disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist,
-                                                     cond, C, D)
+                                                     cond, C, D, keys=keys)
         elif emu:
             dpd = ctx.disp_per_dist_dev(te_raw.data_ptr(), te_f.data_ptr(),
                                         te_dist.data_ptr(), e_n, R, cond, C, D)
@@ -1268,10 +1283,13 @@ def run_cfg3(args, world, rank, local, dist, ctx, dev, peaks=None):
                       'chromosomes), LRT on own chromosomes, genome-wide BH '
                       'as a sample sort over the ranks' if per_pass else
                       'distance re-shard (LPT distance owners, all_to_all of '
-                      'the disp pixels, single-GPU driver per rank, table '
-                      'all-reduce), LRT on own chromosomes, genome-wide BH '
+                      'the disp pixels as %s, single-GPU driver per rank, '
+                      'table all-reduce), LRT on own chromosomes, genome-wide BH '
                       'as a sample sort over the ranks (two all_to_alls of '
-                      'the p-values)'), 'strong', peaks=peaks)
+                      'the p-values)' % ('15-byte key records, f rebuilt on '
+                                         'arrival' if compact else
+                                         '52-byte raw / f / dist records')),
+        'strong', peaks=peaks)
     out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
     out['config']['chromosomes_rank0'] = [int(i) for i in mine]
     out['config']['generate_s_rank0'] = gen_s

@@ -35,6 +35,7 @@ EXPORTS = [
     'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
     'h3d_disp_pixels_dev', 'h3d_table_gather_dev', 'h3d_disp_seg_stats',
     'h3d_scale_disp_dev', 'h3d_npz_backend', 'h3d_npz_csr_read_slack',
+    'h3d_pixel_f_dev',
 ]
 
 
@@ -107,6 +108,8 @@ def load_library(path=None):
             'h3d_disp_pixels_dev': (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _P,
                                          _I64, _I, _I64, _P, _P, _P]),
             'h3d_table_gather_dev': (_I, [_P, _P, _I, _I, _P, _I64, _P]),
+            'h3d_pixel_f_dev': (_I, [_P, _P, _P, _P, _P, _I64, _I, _P, _P, _P,
+                                     _P, _I, _P]),
             'h3d_scale_disp_dev': (_I, [_P, _P, _P, _I, _P, _P, _I64, _I, _I,
                                         _P, ctypes.c_double, _I, _P, _P, _P,
                                         _P]),
@@ -389,6 +392,15 @@ class Context(object):
             n, R, n_disp, _P(d_raw_out) if d_raw_out else None,
             _P(d_f_out) if d_f_out else None,
             _P(d_dist_out) if d_dist_out else None), 'h3d_disp_pixels_dev')
+
+    def pixel_f_dev(self, d_row, d_dist, d_chrom, d_sfi, n, R, d_bias, d_boff,
+                    d_sf, d_soff, nchrom, d_f_out):
+        """f of re-sharded pixels from their keys (h3d_pixel_f_dev): device
+        pointers in and out, synchronous."""
+        _check(self.lib.h3d_pixel_f_dev(
+            self.handle, _P(d_row), _P(d_dist), _P(d_chrom), _P(d_sfi), n, R,
+            _P(d_bias), _P(d_boff), _P(d_sf), _P(d_soff), nchrom,
+            _P(d_f_out)), 'h3d_pixel_f_dev')
 
     def disp_seg_stats(self, D, C):
         """(qcml iterations, Brent NLL evaluations) per segment (D, C) of

@@ -263,8 +263,15 @@ class AnalyzingHiC3DeFDR(object):
         try:
             with torch.cuda.stream(stream):
                 if os.environ.get('H3D_DISP_SHARD') != 'pass':
+                    # the keys of f travel instead of f (15-byte records at
+                    # R = 4; H3D_RESHARD_FULL=1: the full 52-byte record)
+                    keys = None if os.environ.get('H3D_RESHARD_FULL') == '1' \
+                        else self._resident().disp_keys(
+                            self._shards().mine,
+                            {c: i for i, c in enumerate(self.chroms)})
                     return parallel.disp_per_dist_by_distance(
-                        ctx, t_raw, t_f, t_dist, self._cond_of_rep(), C, D)
+                        ctx, t_raw, t_f, t_dist, self._cond_of_rep(), C, D,
+                        keys=keys)
                 return ctx.disp_per_dist_dev(
                     t_raw.data_ptr(), t_f.data_ptr(), t_dist.data_ptr(),
                     t_raw.shape[0], self.design.shape[0], self._cond_of_rep(),

@@ -265,6 +265,44 @@ class Resident(object):
                 torch.empty((n, C), dtype=torch.float64, device=self.dev),
                 np.empty((3, n)), np.empty((n, C)))
 
+    def disp_keys(self, chroms, index):
+        """parallel.PixelKeys of disp_pixels(chroms)' pixels, in the same
+        order: each pixel's row, its chromosome's genome index (``index``:
+        name -> index, the same on every rank) and its row of the
+        chromosome's size-factor table -- the distinct size-factor rows of
+        its disp pixels (torch.unique; a conditional norm has one per
+        distance bin, a global one a single row) -- with every chromosome's
+        filtered bias and that table: what the distance re-shard ships
+        instead of f (h3d_pixel_f_dev rebuilds it bit for bit)."""
+        from hic3defdr_amd import parallel
+        torch = self.torch
+        rows, gs, sfis, tables = [], [], [], {}
+        for c in chroms:
+            e = self.chrom(c)
+            g = int(index[c])
+            if e.sf_per_rep:
+                tab = e.sf.reshape(1, -1)
+            else:
+                sel = e.disp_idx.bool()
+                tab, inv = torch.unique(e.sf[sel], dim=0, return_inverse=True)
+            tables[g] = (np.asarray(e.bias, dtype=np.float64),
+                         tab.cpu().numpy())
+            if not e.n_disp:
+                continue
+            sel = e.disp_idx.bool()
+            rows.append(e.row[sel].to(torch.int32))
+            gs.append(torch.full((e.n_disp,), g, dtype=torch.int32,
+                                 device=self.dev))
+            sfis.append(torch.zeros(e.n_disp, dtype=torch.int32,
+                                    device=self.dev) if e.sf_per_rep
+                        else inv.reshape(-1).to(torch.int32))
+
+        def cat(parts):
+            return torch.cat(parts) if parts else \
+                torch.zeros(0, dtype=torch.int32, device=self.dev)
+        return parallel.PixelKeys(cat(rows), cat(gs), cat(sfis), tables,
+                                  len(index))
+
     def start_session(self, chroms, t_raw, t_f, t_dist, offsets, t_tab, D, C,
                       lrt_bufs=None):
         """estimate_disp's resident result for lrt: its pixels and device

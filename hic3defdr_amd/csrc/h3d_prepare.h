@@ -386,6 +386,48 @@ static __global__ void k_disp_pixels(const int32_t* __restrict__ sel, int64_t n_
   }
 }
 
+// f of re-sharded pixels rebuilt on the rank that receives them (the distance
+// re-shard, parallel.disp_per_dist_by_distance): the sender ships (row,
+// distance, chromosome, size-factor row) instead of f's 8R bytes, every rank
+// holds the genome's bias rows (boff: chromosome g's first row, g + 1's
+// bounds it) and size-factor rows (soff), and f is the product
+// k_disp_pixels forms, in its order: (bias[row] * bias[row + d]) * sf -- so
+// the rebuilt f is the sender's bit for bit. A key outside the tables
+// (chromosome, row + d or the size-factor row) gives NaN and sets *bad.
+static __global__ void k_pixel_f(const int32_t* __restrict__ row,
+                                 const int32_t* __restrict__ dist,
+                                 const int32_t* __restrict__ chrom,
+                                 const int32_t* __restrict__ sfi, int64_t n, int R,
+                                 const double* __restrict__ bias,
+                                 const int64_t* __restrict__ boff,
+                                 const double* __restrict__ sf,
+                                 const int64_t* __restrict__ soff, int nchrom,
+                                 double* __restrict__ f_out, int* __restrict__ bad) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int g = chrom[j];
+    const int64_t r0 = row[j], c0 = r0 + dist[j], s = sfi[j];
+    bool ok = g >= 0 && g < nchrom;
+    int64_t b0 = 0, nb = 0, s0 = 0, ns = 0;
+    if (ok) {
+      b0 = boff[g];
+      nb = boff[g + 1] - b0;
+      s0 = soff[g];
+      ns = soff[g + 1] - s0;
+      ok = r0 >= 0 && r0 <= c0 && c0 < nb && s >= 0 && s < ns;
+    }
+    if (!ok) {
+      for (int k = 0; k < R; ++k) f_out[j * R + k] = NAN;
+      atomicOr(bad, 1);
+      continue;
+    }
+    for (int k = 0; k < R; ++k) {
+      const double bb = bias[(b0 + r0) * R + k] * bias[(b0 + c0) * R + k];
+      f_out[j * R + k] = bb * sf[(s0 + s) * R + k];
+    }
+  }
+}
+
 // prepare_data's scaled and disp_idx (analysis.py:109-115):
 //   scaled = balanced / size_factors,
 //   mean = np.dot(scaled, design) / n_c,

@@ -254,6 +254,33 @@ int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col
   return 0;
 }
 
+int h3d_pixel_f_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_dist,
+                    const int32_t* d_chrom, const int32_t* d_sfi, int64_t n, int R,
+                    const double* d_bias, const int64_t* d_boff, const double* d_sf,
+                    const int64_t* d_soff, int nchrom, double* d_f_out) {
+  if (!ctx) return fail(H3D_EARG, "null argument");
+  if (R < 1 || R > kMaxReps || n < 0 || nchrom < 1)
+    return fail(H3D_EARG, "R=%d n=%lld nchrom=%d", R, (long long)n, nchrom);
+  if (n == 0) return 0;
+  if (!d_row || !d_dist || !d_chrom || !d_sfi || !d_bias || !d_boff || !d_sf || !d_soff ||
+      !d_f_out)
+    return fail(H3D_EARG, "null device pointer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  int* d_bad = (int*)scratch(ctx, "pf_bad", 4);
+  if (!d_bad) return fail(H3D_ENOMEM, "pixel f scratch");
+  HIP_TRY(hipMemsetAsync(d_bad, 0, 4, s));
+  hipLaunchKernelGGL(k_pixel_f, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_row, d_dist,
+                     d_chrom, d_sfi, n, R, d_bias, d_boff, d_sf, d_soff, nchrom, d_f_out,
+                     d_bad);
+  HIP_TRY(hipGetLastError());
+  int bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (bad) return fail(H3D_EINPUT, "pixel keys outside the bias / size-factor tables");
+  return 0;
+}
+
 int h3d_scale_disp_dev(h3d_ctx* ctx, const double* d_balanced, const double* d_sf,
                        int sf_per_rep, const int32_t* d_row, const int32_t* d_col, int64_t n,
                        int R, int C, const uint8_t* design, double mean_thresh,

@@ -17,8 +17,10 @@ over the ranks (``bh_sharded``).
   other, so the pixels are re-sharded by DISTANCE for this stage
   (``disp_per_dist_by_distance``): the distances go to ranks by LPT on
   their genome-wide pixel counts (one all-reduce of a D-long count vector,
-  ``distance_owners``), one all_to_all moves every disp pixel (raw, f,
-  dist: 12 R + 4 bytes) to the rank owning its distance, each rank runs the
+  ``distance_owners``), one all_to_all moves every disp pixel (raw, row,
+  dist, chromosome, size-factor row: 15 bytes at R = 4; f is rebuilt from
+  them bit for bit on arrival, ``exchange_compact``) to the rank owning its
+  distance, each rank runs the
   single-GPU driver -- every Brent search in-kernel -- on the distances it
   owns, and one all-reduce of the D x C table (owners' rows, zeros
   elsewhere) gives every rank the same disp_per_dist. The only change from
@@ -113,26 +115,31 @@ def _split(m, k, j):
     return m * (j + 1) // k - m * j // k
 
 
-def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
-    """Moves every pixel (raw (n, R) int32, f (n, R) float64, dist (n,)
-    int32) to the rank ``owner`` (n,) names, as one byte record per pixel
-    (raw 4R | f 8R | dist 4). Returns this rank's received (raw, f, dist):
-    the pixels of source rank 0 first, each source's in its own order.
+def exchange_columns(cols, owner, group=None, chunks=1):
+    """Moves pixel i of every column in ``cols`` (tensors of n rows: (n,) or
+    (n, k), any dtype, one device) to the rank ``owner[i]`` names, packed as
+    one byte record per pixel (the columns' bytes side by side). Returns this
+    rank's received columns (same dtypes and trailing shapes): the pixels of
+    source rank 0 first, each source's in its own order.
 
     ``chunks`` > 1: every destination's block is cut into that many parts
     and part j of all blocks goes in its own all_to_all_single, issued
     asynchronously -- the packing of part j + 1 (a gather on the device)
     runs while part j is on the wire, and the receiving rank places each
     part at its offset, so the result is the one-shot exchange's bit for
-    bit (tests/test_dist_gloo.py)."""
+    bit (tests/test_dist_gloo.py). Every rank issues the same number of
+    collectives, pixels or not."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    dev = t_raw.device
+    dev = cols[0].device
     xdev = _xdev(dev, group)
-    n, R = t_raw.shape
-    width = 12 * R + 4
+    n = int(cols[0].shape[0])
+    tails = [tuple(c.shape[1:]) for c in cols]
+    widths = [int(np.prod(t, dtype=np.int64)) * c.element_size()
+              for t, c in zip(tails, cols)]
+    width = int(sum(widths))
     order = torch.argsort(owner, stable=True)
 
     def as_bytes(t, w):
@@ -145,10 +152,8 @@ def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
     dist.all_to_all_single(recv, send.to(xdev), group=group)
     s_list, r_list = send.tolist(), recv.tolist()
     m = int(sum(r_list))
-    # every rank issues the same number of collectives, pixels or not (a
-    # rank with n == m == 0 sends and receives empty parts)
     k = max(1, int(chunks))
-    cols = [as_bytes(t_raw, 4 * R), as_bytes(t_f, 8 * R), as_bytes(t_dist, 4)]
+    bcols = [as_bytes(c, w) for c, w in zip(cols, widths)]
     s_off = np.concatenate([[0], np.cumsum(s_list)])
     r_off = np.concatenate([[0], np.cumsum(r_list)])
     works, parts = [], []
@@ -159,7 +164,7 @@ def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
         idx = torch.cat([order[int(s_off[d]) + s_list[d] * j // k:
                                int(s_off[d]) + s_list[d] * j // k + ss[d]]
                          for d in range(world)]) if n else order[:0]
-        rec = torch.cat([c[idx] for c in cols], dim=1).to(xdev)
+        rec = torch.cat([c[idx] for c in bcols], dim=1).to(xdev)
         got = torch.empty((int(sum(rs)), width), dtype=torch.uint8,
                           device=xdev)
         works.append(dist.all_to_all_single(
@@ -175,15 +180,144 @@ def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
             out[a:a + rs[d]] = got[pos:pos + rs[d]]
             pos += rs[d]
     out = out.to(dev)
+    res, pos = [], 0
+    for c, t, w in zip(cols, tails, widths):
+        if m:
+            res.append(out[:, pos:pos + w].contiguous().view(c.dtype)
+                       .reshape((m,) + t))
+        else:
+            res.append(torch.empty((0,) + t, dtype=c.dtype, device=dev))
+        pos += w
+    return res
+
+
+def exchange_by_owner(t_raw, t_f, t_dist, owner, group=None, chunks=1):
+    """exchange_columns of (raw (n, R) int32, f (n, R) float64, dist (n,)
+    int32): one 12 R + 4 byte record per pixel (the full record; the
+    distance re-shard ships the keys of f instead when it has them,
+    exchange_compact)."""
+    return tuple(exchange_columns([t_raw, t_f, t_dist], owner, group,
+                                  chunks))
+
+
+class PixelKeys(object):
+    """What the distance re-shard ships instead of a disp pixel's f
+    (8 R bytes): the keys f is rebuilt from on the receiving rank, bit for
+    bit -- f = (bias[row] * bias[row + dist]) * sf (h3d_disp_pixels_dev's
+    product, analysis.py:181) -- plus this rank's tables.
+
+    row, chrom, sfi: (n,) int32 tensors on the pixels' device: the pixel's
+    bin row, its chromosome's index in the genome (0 .. nchrom - 1, the same
+    on every rank), the row of its chromosome's size-factor table.
+    tables: {chromosome index: (bias (n_bins, R), size-factor rows (S, R))}
+    for this rank's chromosomes (host float64; the bias filtered as
+    core.load_bias). ``device_tables`` stacks every rank's (one all-reduce of
+    the sizes, one of the rows; cached)."""
+
+    def __init__(self, row, chrom, sfi, tables, nchrom):
+        self.row, self.chrom, self.sfi = row, chrom, sfi
+        self.tables = tables
+        self.nchrom = int(nchrom)
+        self._dev = None
+
+    def device_tables(self, dev, R, group=None):
+        """(bias (B, R), boff (nchrom + 1), sf (S, R), soff (nchrom + 1)) on
+        ``dev``, every rank's chromosomes stacked in genome order: each
+        chromosome is held by one rank, the others contribute zeros to the
+        two sums (x + 0 = x: the rows arrive bit for bit)."""
+        import torch
+        import torch.distributed as dist
+        if self._dev is not None:
+            return self._dev
+        xdev = _xdev(dev, group)
+        G = self.nchrom
+        sizes = np.zeros(2 * G, dtype=np.int64)
+        for g, (b, s) in self.tables.items():
+            sizes[g], sizes[G + g] = len(b), len(s)
+        t_sizes = torch.from_numpy(sizes).to(xdev)
+        dist.all_reduce(t_sizes, op=dist.ReduceOp.SUM, group=group)
+        sizes = t_sizes.cpu().numpy()
+        boff = np.concatenate([[0], np.cumsum(sizes[:G])]).astype(np.int64)
+        soff = np.concatenate([[0], np.cumsum(sizes[G:])]).astype(np.int64)
+        rows = np.zeros((int(boff[-1] + soff[-1]), R))
+        for g, (b, s) in self.tables.items():
+            rows[boff[g]:boff[g + 1]] = b
+            rows[boff[-1] + soff[g]:boff[-1] + soff[g + 1]] = s
+        t_rows = torch.from_numpy(rows).to(xdev)
+        dist.all_reduce(t_rows, op=dist.ReduceOp.SUM, group=group)
+        t_rows = t_rows.to(dev)
+        nb = int(boff[-1])
+        self._dev = (t_rows[:nb].contiguous(),
+                     torch.from_numpy(boff).to(dev),
+                     t_rows[nb:].contiguous(),
+                     torch.from_numpy(soff).to(dev))
+        return self._dev
+
+
+def _narrowest(vmax):
+    """The narrowest integer dtype holding 0 .. vmax."""
+    import torch
+    for dt, top in ((torch.uint8, 255), (torch.int16, 32767)):
+        if vmax <= top:
+            return dt
+    return torch.int32
+
+
+def exchange_compact(ctx, t_raw, t_dist, keys, owner, group=None, chunks=1):
+    """The distance re-shard's pixel exchange with f rebuilt on arrival: one
+    record per pixel of raw (R counts), row, dist, chromosome and
+    size-factor row, each column in the narrowest integer width that holds
+    every rank's values (one all-reduce of the four maxima; the escape to a
+    wider column is automatic) -- R = 4, counts < 2^15, D <= 256, <= 256
+    chromosomes and size-factor rows: 15 bytes against the full record's 52
+    -- then f by h3d_pixel_f_dev from the
+    stacked bias / size-factor tables (PixelKeys.device_tables). Returns the
+    received (raw (m, R) int32, f (m, R) float64, dist (m,) int32), bit for
+    bit what exchange_by_owner delivers."""
+    import torch
+    import torch.distributed as dist
+    dev = t_raw.device
+    xdev = _xdev(dev, group)
+    n, R = t_raw.shape
+    tabs = keys.device_tables(dev, R, group)
+    mx = torch.zeros(4, dtype=torch.int64, device=dev)
+    if n:
+        mx = torch.stack([t_raw.max().long(), t_dist.max().long(),
+                          keys.chrom.max().long(), keys.sfi.max().long()])
+    lo = min(int(t_raw.min()), int(t_dist.min()), int(keys.chrom.min()),
+             int(keys.sfi.min())) if n else 0
+    if lo < 0:
+        raise ValueError('exchange_compact: negative count, distance or key')
+    mx = mx.to(xdev)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    w = [_narrowest(int(v)) for v in mx.tolist()]
+    cols = [t_raw.to(w[0]), keys.row.to(torch.int32), t_dist.to(w[1]),
+            keys.chrom.to(w[2]), keys.sfi.to(w[3])]
+    raw_m, row_m, dist_m, chrom_m, sfi_m = exchange_columns(cols, owner,
+                                                            group, chunks)
+    m = int(raw_m.shape[0])
+    raw_m = raw_m.to(torch.int32)
+    dist_m = dist_m.to(torch.int32).contiguous()
+    f_m = torch.empty((m, R), dtype=torch.float64, device=dev)
     if m:
-        raw_m = out[:, :4 * R].contiguous().view(torch.int32).reshape(m, R)
-        f_m = out[:, 4 * R:12 * R].contiguous().view(torch.float64).reshape(m, R)
-        dist_m = out[:, 12 * R:].contiguous().view(torch.int32).reshape(m)
-    else:
-        raw_m = torch.empty((0, R), dtype=torch.int32, device=dev)
-        f_m = torch.empty((0, R), dtype=torch.float64, device=dev)
-        dist_m = torch.empty(0, dtype=torch.int32, device=dev)
-    return raw_m, f_m, dist_m
+        row_m = row_m.contiguous()
+        chrom_m = chrom_m.to(torch.int32).contiguous()
+        sfi_m = sfi_m.to(torch.int32).contiguous()
+        ctx.pixel_f_dev(row_m.data_ptr(), dist_m.data_ptr(),
+                        chrom_m.data_ptr(), sfi_m.data_ptr(), m, R,
+                        tabs[0].data_ptr(), tabs[1].data_ptr(),
+                        tabs[2].data_ptr(), tabs[3].data_ptr(), keys.nchrom,
+                        f_m.data_ptr())
+    return raw_m.contiguous(), f_m, dist_m
+
+
+def compact_record_bytes(R, raw_max, dist_max, nchrom, sf_rows):
+    """Bytes of one exchange_compact record (the model of
+    tools/emulate_ranks.py)."""
+    import torch
+    sz = [torch.empty(0, dtype=_narrowest(v)).element_size()
+          for v in (raw_max, dist_max, nchrom - 1, sf_rows - 1)]
+    return R * sz[0] + 4 + sz[1] + sz[2] + sz[3]
 
 
 # parts of the distance re-shard's all_to_all (H3D_RESHARD_CHUNKS): the
@@ -192,16 +326,19 @@ RESHARD_CHUNKS = int(os.environ.get('H3D_RESHARD_CHUNKS', '4'))
 
 
 def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
-                              group=None, chunks=None):
+                              group=None, chunks=None, keys=None):
     """estimate_disp's (D, C) disp_per_dist over every rank's pixels: the
     distances go to ranks by LPT on their genome-wide pixel counts (one
     all-reduce of D counts), the pixels move to the rank owning their
-    distance (exchange_by_owner: the all_to_all in ``chunks`` asynchronous
-    parts), each rank runs the single-GPU driver on what it received, and
-    ONE all-reduce of the owners' rows gives every rank the whole table.
+    distance (the all_to_all in ``chunks`` asynchronous parts), each rank
+    runs the single-GPU driver on what it received, and ONE all-reduce of
+    the owners' rows gives every rank the whole table.
 
     t_raw (n, R) int32, t_f (n, R) float64, t_dist (n,) int32: this rank's
-    disp pixels on its GPU. libh3d must run on torch's current stream (a real
+    disp pixels on its GPU. ``keys`` (PixelKeys): ship the keys of f instead
+    of f (exchange_compact: 15-byte records at R = 4 instead of 52, f rebuilt
+    bit for bit on arrival); without them the full record
+    (exchange_by_owner). libh3d must run on torch's current stream (a real
     one: see make_allreduce). Returns the table as a (D, C) numpy array."""
     import torch
     import torch.distributed as dist
@@ -219,9 +356,13 @@ def disp_per_dist_by_distance(ctx, t_raw, t_f, t_dist, cond_of_rep, C, D,
     # distances outside [0, D) go to rank 0, whose driver rejects them
     owner = torch.zeros(n, dtype=torch.int64, device=dev)
     owner[inb] = torch.from_numpy(owner_of.astype(np.int64)).to(dev)[dl[inb]]
-    raw_m, f_m, dist_m = exchange_by_owner(
-        t_raw, t_f, t_dist, owner, group,
-        RESHARD_CHUNKS if chunks is None else chunks)
+    k = RESHARD_CHUNKS if chunks is None else chunks
+    if keys is not None:
+        raw_m, f_m, dist_m = exchange_compact(ctx, t_raw, t_dist, keys, owner,
+                                              group, k)
+    else:
+        raw_m, f_m, dist_m = exchange_by_owner(t_raw, t_f, t_dist, owner,
+                                               group, k)
     m = int(raw_m.shape[0])
     tab = ctx.disp_per_dist_dev(raw_m.data_ptr(), f_m.data_ptr(),
                                 dist_m.data_ptr(), m, R, cond_of_rep, C, D)

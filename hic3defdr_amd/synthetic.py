@@ -184,7 +184,7 @@ def write_genome(base, bins, seed=3, workers=8, dmax=200, n_per_cond=(2, 2)):
 
 
 def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05,
-              workers=8):
+              workers=8, keys=False):
     """The disp pixels of one chromosome drawn directly in the distance band,
     no files (the cfg3 / cfg4 shapes, where writing NPZ files for a whole
     genome would dominate): the generator model above with unit size
@@ -196,7 +196,9 @@ def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05,
     per replicate (SeedSequence children), the replicates drawn on `workers`
     threads (numpy's bulk draws release the GIL) -- so a rank can draw just
     its own chromosomes and every world size sees the same genome. Returns
-    (raw (n, R) int32, f (n, R) f64, dist (n,) int32)."""
+    (raw (n, R) int32, f (n, R) f64, dist (n,) int32); with ``keys`` also
+    (row (n,) int32, bias (n_bins, R)): f = (bias[row] * bias[row + dist])
+    * 1 (unit size factors), what the distance re-shard rebuilds f from."""
     import concurrent.futures
     R = int(sum(n_per_cond))
     kids = np.random.SeedSequence([seed, chrom_index]).spawn(R + 1)
@@ -213,11 +215,13 @@ def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05,
     diff = rng.random(d.size) < 0.01
     raw = np.empty((d.size, R), dtype=np.int32)
     f = np.empty((d.size, R))
+    bias = np.empty((n_bins, R))
     n = 1.0 / disp
 
     def replicate(k):
         g = np.random.default_rng(kids[k + 1])
         b = np.exp(g.normal(0, 0.25, n_bins))
+        bias[:, k] = b
         bb = b[r] * b[c]
         mu = base * np.where(diff & (cond[k] >= 1), 2.0, 1.0) * bb * \
             (0.8 + 0.1 * (k % 4))
@@ -228,12 +232,15 @@ def draw_band(n_bins, n_per_cond, dmax, seed=0, chrom_index=0, disp=0.05,
     keep = d >= 4
     for ci in range(len(n_per_cond)):
         keep &= (raw[:, cond == ci] / f[:, cond == ci]).mean(axis=1) >= 1.0
-    return (np.ascontiguousarray(raw[keep]), np.ascontiguousarray(f[keep]),
-            np.ascontiguousarray(d[keep]))
+    out = (np.ascontiguousarray(raw[keep]), np.ascontiguousarray(f[keep]),
+           np.ascontiguousarray(d[keep]))
+    if keys:
+        out += (np.ascontiguousarray(r[keep]), bias)
+    return out
 
 
 def draw_genome(bins_list, n_per_cond, dmax, seed=0, indices=None,
-                workers=8):
+                workers=8, keys=False):
     """draw_band for the chromosomes `indices` (default all) of a genome
     given as a list of bin counts, drawn concurrently (each chromosome has
     its own generator; numpy draws release the GIL). Returns the list of
@@ -245,5 +252,5 @@ def draw_genome(bins_list, n_per_cond, dmax, seed=0, indices=None,
         # (the chromosomes in parallel, each one's replicates serially)
         return list(ex.map(lambda i: draw_band(bins_list[i], n_per_cond, dmax,
                                                seed=seed, chrom_index=i,
-                                               workers=1),
+                                               workers=1, keys=keys),
                            idx))

@@ -196,6 +196,21 @@ int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col
                         int64_t n, int R, int64_t n_disp, int32_t* d_raw_out,
                         double* d_f_out, int32_t* d_dist_out);
 
+/* f of pixels received by the distance re-shard, rebuilt from their keys
+ * (replaces shipping f; analysis.py:169-183 forms it on the rank that
+ * prepared the chromosome): pixel j of genome chromosome d_chrom[j] at
+ * (d_row[j], d_row[j] + d_dist[j]) with size-factor row d_sfi[j] gets
+ * d_f_out[j, k] = (bias[row, k] * bias[col, k]) * sf[sfi, k] -- the product
+ * and order of h3d_disp_pixels_dev, so bit for bit the sender's f. d_bias
+ * (B, R): every chromosome's (filtered) bias rows stacked, chromosome g's
+ * from d_boff[g] (nchrom + 1 offsets); d_sf (S, R) its size-factor rows from
+ * d_soff[g]. A key outside its chromosome's rows is H3D_EINPUT (its f NaN).
+ * Synchronous. */
+int h3d_pixel_f_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_dist,
+                    const int32_t* d_chrom, const int32_t* d_sfi, int64_t n, int R,
+                    const double* d_bias, const int64_t* d_boff, const double* d_sf,
+                    const int64_t* d_soff, int nchrom, double* d_f_out);
+
 /* ---- estimate_disp ----------------------------------------------------- */
 
 /* Per-(distance, condition) dispersion (analysis.py:185-206). raw/f (n, R),

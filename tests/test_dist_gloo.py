@@ -133,6 +133,25 @@ class _HostCtx(object):
         dist_ = arr(d_dist, ctypes.c_int32, n)
         return _rounds(raw, f, dist_, np.asarray(cond_of_rep))
 
+    def pixel_f_dev(self, d_row, d_dist, d_chrom, d_sfi, n, R, d_bias, d_boff,
+                    d_sf, d_soff, nchrom, d_f_out):
+        """h3d_pixel_f_dev's product, (bias[row] * bias[col]) * sf, in
+        numpy on the host tensors behind the addresses."""
+        def view(ptr, ctype, count):
+            buf = (ctype * count).from_address(ptr)
+            return np.frombuffer(buf, dtype=np.dtype(ctype))
+        row = view(d_row, ctypes.c_int32, n)
+        dist_ = view(d_dist, ctypes.c_int32, n)
+        g = view(d_chrom, ctypes.c_int32, n)
+        sfi = view(d_sfi, ctypes.c_int32, n)
+        boff = view(d_boff, ctypes.c_int64, nchrom + 1)
+        soff = view(d_soff, ctypes.c_int64, nchrom + 1)
+        bias = view(d_bias, ctypes.c_double, int(boff[-1]) * R).reshape(-1, R)
+        sf = view(d_sf, ctypes.c_double, int(soff[-1]) * R).reshape(-1, R)
+        out = view(d_f_out, ctypes.c_double, n * R).reshape(n, R)
+        r0 = boff[g] + row
+        out[...] = bias[r0] * bias[r0 + dist_] * sf[soff[g] + sfi]
+
 
 def _reshard_worker(rank, world, tmp, port, result_file):
     import torch
@@ -257,8 +276,9 @@ def _genome_worker(rank, world, port, result_file):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     mine = parallel.lpt_assign({i: b for i, b in enumerate(GENOME)},
                                world)[rank]
+    mine = sorted(mine)
     parts = synthetic.draw_genome(GENOME, (2, 2), D - 1, seed=4,
-                                  indices=sorted(mine))
+                                  indices=mine, keys=True)
     raw = np.concatenate([p[0] for p in parts])
     f = np.concatenate([p[1] for p in parts])
     d = np.concatenate([p[2] for p in parts])
@@ -266,6 +286,18 @@ def _genome_worker(rank, world, port, result_file):
     tab = parallel.disp_per_dist_by_distance(
         _HostCtx(), torch.from_numpy(raw), torch.from_numpy(f),
         torch.from_numpy(d), cond, 2, D)
+    # the bench's compact re-shard: the keys of f (unit size factors)
+    keys = parallel.PixelKeys(
+        torch.from_numpy(np.concatenate([p[3] for p in parts])),
+        torch.from_numpy(np.concatenate([np.full(len(p[0]), i, np.int32)
+                                         for i, p in zip(mine, parts)])),
+        torch.zeros(len(raw), dtype=torch.int32),
+        {i: (p[4], np.ones((1, 4))) for i, p in zip(mine, parts)},
+        len(GENOME))
+    tab_keys = parallel.disp_per_dist_by_distance(
+        _HostCtx(), torch.from_numpy(raw), torch.from_numpy(f),
+        torch.from_numpy(d), cond, 2, D, keys=keys)
+    np.testing.assert_array_equal(tab_keys, tab)
     # p-values stand-in: a deterministic function of each pixel's counts
     p = torch.from_numpy((raw[:, 0] % 97 + 0.5) / 97.0 * 0.3)
     q = parallel.bh_all_ranks(
@@ -431,3 +463,87 @@ def test_chunked_reshard_equals_one_shot(world, idle):
             for c in range(3):
                 for j in range(3):
                     np.testing.assert_array_equal(got[3 * c + j], want[j])
+
+
+def _keys_for(kw, data, mine, R):
+    """PixelKeys of this rank's chromosomes (genome index = position in
+    CHROMS): row, chromosome, size-factor row (np.unique of the disp
+    pixels' size-factor rows) and the (bias, size-factor rows) tables."""
+    import torch
+    names = list(CHROMS)
+    rows, chroms, sfis, tables = [], [], [], {}
+    for c in mine:
+        prep, bias = data[c][0], data[c][1]
+        di = prep['disp_idx']
+        sf = prep['size_factors'][di]
+        uniq, inv = np.unique(sf, axis=0, return_inverse=True)
+        g = names.index(c)
+        rows.append(prep['row'][di].astype(np.int32))
+        chroms.append(np.full(int(di.sum()), g, dtype=np.int32))
+        sfis.append(inv.reshape(-1).astype(np.int32))
+        tables[g] = (bias, uniq)
+    cat = (lambda a: torch.from_numpy(np.concatenate(a) if a else
+                                      np.zeros(0, np.int32)))
+    return parallel.PixelKeys(cat(rows), cat(chroms), cat(sfis), tables,
+                              len(names))
+
+
+def _compact_worker(rank, world, tmp, port, result_file):
+    import torch
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    kw, data = _prep(os.path.join(tmp, 'r%d' % rank))
+    mine = parallel.lpt_assign({c: len(data[c][2]) for c in CHROMS},
+                               world)[rank]
+    R = kw['design'].shape[0]
+    raw = np.concatenate([data[c][2] for c in mine] or
+                         [np.zeros((0, R), np.int32)])
+    f = np.concatenate([data[c][3] for c in mine] or [np.zeros((0, R))])
+    dist_ = np.concatenate([data[c][4] for c in mine] or
+                           [np.zeros(0, np.int32)])
+    t_raw = torch.from_numpy(np.ascontiguousarray(raw, np.int32))
+    t_f = torch.from_numpy(np.ascontiguousarray(f))
+    t_dist = torch.from_numpy(np.ascontiguousarray(dist_, np.int32))
+    keys = _keys_for(kw, data, mine, R)
+    owner = torch.from_numpy((dist_ * 7 % world).astype(np.int64))
+    full = parallel.exchange_by_owner(t_raw, t_f, t_dist, owner, chunks=3)
+    comp = parallel.exchange_compact(_HostCtx(), t_raw, t_dist, keys, owner,
+                                     chunks=3)
+    cond = kw['design'].argmax(axis=1).astype(np.int32)
+    C = kw['design'].shape[1]
+    tab_full = parallel.disp_per_dist_by_distance(
+        _HostCtx(), t_raw, t_f, t_dist, cond, C, D)
+    tab_comp = parallel.disp_per_dist_by_distance(
+        _HostCtx(), t_raw, t_f, t_dist, cond, C, D, keys=keys)
+    np.savez(result_file % rank, *[t.numpy() for t in full + comp],
+             tab_full=tab_full, tab_comp=tab_comp)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_compact_reshard_equals_full_record(world):
+    """The distance re-shard's compact exchange (parallel.exchange_compact:
+    raw / row / dist / chromosome / size-factor row in their narrowest
+    widths, f rebuilt on arrival from the stacked bias and size-factor
+    tables) delivers raw, f and dist bit for bit as the full 52-byte record
+    does, and disp_per_dist_by_distance gives the same table either way
+    (world 3 > 2 chromosomes: one rank holds no chromosome)."""
+    h3dbuild.build_hosttest()
+    with tempfile.TemporaryDirectory() as tmp:
+        res = os.path.join(tmp, 'c_%d.npz')
+        port = 29300 + (os.getpid() % 1000) + world
+        mp.spawn(_compact_worker, args=(world, tmp, port, res), nprocs=world,
+                 join=True)
+        for r in range(world):
+            z = np.load(res % r)
+            for j in range(3):
+                a, b = z['arr_%d' % j], z['arr_%d' % (3 + j)]
+                assert a.dtype == b.dtype and a.shape == b.shape
+                np.testing.assert_array_equal(a, b)
+            np.testing.assert_array_equal(z['tab_full'], z['tab_comp'])
+    assert parallel.compact_record_bytes(4, 30000, 250, 20, 40) == 15
+    assert parallel.compact_record_bytes(4, 1 << 20, 250, 20, 40) == 23
+    assert parallel.compact_record_bytes(4, 30000, 400, 300, 40) == 17

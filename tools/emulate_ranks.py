@@ -30,6 +30,58 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 
+def collectives(parts, assign, counts, N, D, C, rec_bytes, max_ms, ms1,
+                args):
+    """The collectives of one N-GPU cfg3 step (not run: one GPU), from the
+    actual pixel routing: rank r holds the disp pixels of its LPT
+    chromosomes and sends each to the owner of its distance (``rec_bytes``
+    per pixel: parallel.compact_record_bytes, or 12 R + 4 for the full
+    record); BH sends each p-value to its value-range bucket's rank and the q
+    back (8 B each way, ~1/N of a rank's values per peer); the D x C table
+    all-reduce and the small all_gathers / count all-reduces are latency
+    only. On the full xGMI mesh every (source, destination) pair has its own
+    link, so an all_to_all takes about the largest pair's bytes / the link
+    bandwidth. Added serially (no overlap credited) to ``max_ms``, the
+    slowest rank's measured kernel share."""
+    from hic3defdr_amd import parallel
+    owner = parallel.distance_owners(counts, N)
+    pair = np.zeros((N, N))
+    for r in range(N):
+        dr = np.concatenate([parts[i][2] for i in assign[r]]) \
+            if assign[r] else np.zeros(0, dtype=np.int64)
+        pair[r] = np.bincount(owner[dr], minlength=N)[:N] * rec_bytes
+    np.fill_diagonal(pair, 0)
+    n_r = [sum(len(parts[i][2]) for i in assign[r]) for r in range(N)]
+    bh_pair = max(n_r) * 8.0 / N       # ~1/N of a rank's values per peer
+    bw = args.link_gbs * 1e9 * args.link_eff
+    t_pix = pair.max() / bw * 1e3
+    t_bh = 2 * bh_pair / bw * 1e3
+    # counts all-reduce, the record-width max all-reduce, 2 exchange
+    # all_to_alls (sizes + records), table all-reduce, BH: 3 all_gathers +
+    # 2 all_to_alls
+    n_coll = 10
+    t_lat = n_coll * args.latency_us * 1e-3
+    proj = max_ms + t_pix + t_bh + t_lat
+    print('N=%d, %d-byte records: projected %.2f ms (kernels %.2f, pixel '
+          'all_to_all %.2f, BH %.2f, latency %.2f) -> %.2fx (%.1f%%)' % (
+              N, rec_bytes, proj, max_ms, t_pix, t_bh, t_lat, ms1 / proj,
+              100 * ms1 / proj / N), flush=True)
+    return {'record_bytes': rec_bytes,
+            'pixel_all_to_all_max_pair_bytes': float(pair.max()),
+            'pixel_all_to_all_bytes_out_per_rank_max': float(pair.sum(1).max()),
+            'bh_all_to_all_pair_bytes': float(bh_pair),
+            'table_allreduce_bytes': 8 * D * C,
+            'assumed': {'link_GBps_per_direction': args.link_gbs,
+                        'efficiency': args.link_eff,
+                        'latency_us_per_collective': args.latency_us,
+                        'collectives_per_step': n_coll},
+            'ms': {'kernels_slowest_rank': max_ms, 'pixel_all_to_all': t_pix,
+                   'bh_all_to_alls': t_bh, 'latency': t_lat},
+            'projected_step_ms_pixels_owners': proj,
+            'projected_speedup_vs_n1': ms1 / proj,
+            'projected_efficiency': ms1 / proj / N}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--worlds', default='2,4,8')
@@ -42,9 +94,13 @@ def main():
     ap.add_argument('--link-gbs', type=float, default=76.5)
     ap.add_argument('--link-eff', type=float, default=0.6)
     ap.add_argument('--latency-us', type=float, default=30.0)
+    ap.add_argument('--from', dest='from_json', default=None,
+                    help='no GPU: take the measured kernel shares (N = 1 and '
+                         'each world\'s slowest rank, pixel-count owners) '
+                         'from an earlier run\'s JSON and project the '
+                         'collectives for both re-shard records')
     args = ap.parse_args()
-    import torch
-    from hic3defdr_amd import _native, parallel, synthetic
+    from hic3defdr_amd import parallel, synthetic
     bins = synthetic.MM10_BINS
     D = args.dmax + 1
     R, C = 4, 2
@@ -52,14 +108,39 @@ def main():
     t0 = time.perf_counter()
     parts = synthetic.draw_genome(bins, (2, 2), args.dmax, seed=0, workers=16)
     print('drew the genome in %.1f s' % (time.perf_counter() - t0), flush=True)
+    d_all = np.concatenate([p[2] for p in parts])
+    counts = np.bincount(d_all, minlength=D)[:D]
+    # the re-shard's record: the compact one (parallel.exchange_compact:
+    # raw / row / dist / chromosome / size-factor row at their narrowest
+    # widths; the genome's unit size factors are one row) and the full one
+    rec = {'compact': parallel.compact_record_bytes(
+               R, int(max(p[0].max() for p in parts)), args.dmax, len(bins),
+               1),
+           'full': 12 * R + 4}
+    if args.from_json:
+        prev = json.load(open(args.from_json))
+        ms1 = prev['n1']['ms']
+        out = {'from': args.from_json, 'n1_ms': ms1, 'record_bytes': rec,
+               'worlds': {}}
+        for N in [int(v) for v in args.worlds.split(',')]:
+            assign = parallel.lpt_assign({i: b for i, b in enumerate(bins)},
+                                         N)
+            mx = prev['worlds'][str(N)]['pixels']['max_ms']
+            out['worlds'][str(N)] = {
+                kind: collectives(parts, assign, counts, N, D, C, rb, mx, ms1,
+                                  args)
+                for kind, rb in rec.items()}
+        os.makedirs(os.path.dirname(args.out), exist_ok=True)
+        with open(args.out, 'w') as fh:
+            json.dump(out, fh, indent=1)
+        return
+    import torch
+    from hic3defdr_amd import _native
     ctx = _native.context(0)
     dev = torch.device('cuda', 0)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    d_all = np.concatenate([p[2] for p in parts])
-    counts = np.bincount(d_all, minlength=D)[:D]
-
     def up(raw, f, dist):
         return (torch.from_numpy(np.ascontiguousarray(raw, dtype=np.int32)).to(dev),
                 torch.from_numpy(np.ascontiguousarray(f)).to(dev),
@@ -170,51 +251,14 @@ def main():
             print('N=%d owners=%s: max %.2f ms -> %.2fx of N=1 (%.1f%% '
                   'efficiency)' % (N, name, mx, ms1 / mx, 100 * ms1 / mx / N),
                   flush=True)
-        # the collectives (not run: one GPU), per step, from the actual pixel
-        # routing: rank r holds the disp pixels of its LPT chromosomes and
-        # sends each to the owner of its distance (12 R + 4 B records); BH
-        # sends each p-value to its value-range bucket's rank and the q back
-        # (8 B each way, ~1/N of a rank's values per peer); the D x C table
-        # all-reduce and the small all_gathers / count all-reduces are
-        # latency only. On the full xGMI mesh every (source, destination)
-        # pair has its own link, so an all_to_all takes about the largest
-        # pair's bytes / the link bandwidth.
-        owner = parallel.distance_owners(counts, N)
-        pair = np.zeros((N, N))
-        for r in range(N):
-            dr = np.concatenate([parts[i][2] for i in assign[r]]) \
-                if assign[r] else np.zeros(0, dtype=np.int64)
-            pair[r] = np.bincount(owner[dr], minlength=N)[:N] * (12 * R + 4)
-        np.fill_diagonal(pair, 0)
-        n_r = [sum(len(parts[i][2]) for i in assign[r]) for r in range(N)]
-        bh_pair = max(n_r) * 8.0 / N       # ~1/N of a rank's values per peer
-        bw = args.link_gbs * 1e9 * args.link_eff
-        t_pix = pair.max() / bw * 1e3
-        t_bh = 2 * bh_pair / bw * 1e3
-        n_coll = 9   # counts all-reduce, 2 exchange all_to_alls (sizes +
-        # records), table all-reduce, BH: 3 all_gathers + 2 all_to_alls
-        t_lat = n_coll * args.latency_us * 1e-3
         best = min(res[k]['max_ms'] for k in ('pixels', 'measured', 'model'))
-        proj = res['pixels']['max_ms'] + t_pix + t_bh + t_lat
-        res['collectives'] = {
-            'pixel_all_to_all_max_pair_bytes': float(pair.max()),
-            'pixel_all_to_all_bytes_out_per_rank_max': float(pair.sum(1).max()),
-            'bh_all_to_all_pair_bytes': float(bh_pair),
-            'table_allreduce_bytes': 8 * D * C,
-            'assumed': {'link_GBps_per_direction': args.link_gbs,
-                        'efficiency': args.link_eff,
-                        'latency_us_per_collective': args.latency_us,
-                        'collectives_per_step': n_coll},
-            'ms': {'pixel_all_to_all': t_pix, 'bh_all_to_alls': t_bh,
-                   'latency': t_lat},
-            'projected_step_ms_pixels_owners': proj,
-            'projected_speedup_vs_n1': ms1 / proj,
-            'projected_efficiency': ms1 / proj / N,
-            'best_owner_table_max_ms': best}
-        print('N=%d projected with collectives: %.2f ms (pixel all_to_all '
-              '%.2f, BH %.2f, latency %.2f) -> %.2fx (%.1f%%)' % (
-                  N, proj, t_pix, t_bh, t_lat, ms1 / proj,
-                  100 * ms1 / proj / N), flush=True)
+        res['collectives'] = collectives(parts, assign, counts, N, D, C,
+                                         rec['compact'],
+                                         res['pixels']['max_ms'], ms1, args)
+        res['collectives']['best_owner_table_max_ms'] = best
+        res['collectives_full_record'] = collectives(
+            parts, assign, counts, N, D, C, rec['full'],
+            res['pixels']['max_ms'], ms1, args)
         out['worlds'][str(N)] = res
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, 'w') as fh:
