@@ -510,12 +510,7 @@ def cfg3_vs_cpu(ctx, p, dpd, cpu_p, cpu_dpd, dmax):
     fin = np.isfinite(cpu_dpd)
     drel = np.zeros_like(cpu_dpd)
     drel[fin] = np.abs(dpd[fin] - cpu_dpd[fin]) / np.abs(cpu_dpd[fin])
-    segs = [{'distance': int(d), 'condition': int(c),
-             'rel': float(drel[d, c]),
-             'd_delta_over_xatol': float(abs(
-                 dpd[d, c] / (1 + dpd[d, c])
-                 - cpu_dpd[d, c] / (1 + cpu_dpd[d, c])) / 1e-5)}
-            for d, c in zip(*np.nonzero(drel > 1e-6))]
+    segs = segments_vs(dpd, cpu_dpd)
     return {'pixels': int(len(p)),
             'max_rel_dp': float(rel.max()),
             'pixels_rel_dp_gt_1e-6': int(np.sum(rel > 1e-6)),
@@ -558,7 +553,23 @@ def sample_parity(ctx, sample, dmax):
 GOLDEN = os.path.join(REPO, 'tests', 'golden')
 
 
-def parity_vs_reference(ctx, o, n, bins, dmax, seed):
+def segments_vs(dpd, ref, bar=1e-6, xatol=1e-5):
+    """The (distance, condition) segments of ``dpd`` beyond ``bar`` relative
+    of ``ref``, each with its move in delta = disp / (1 + disp) -- the
+    variable of cml's bounded Brent search (dispersion.py:72-80) -- in units
+    of its xatol: a near-tied NLL comparison sends a search to another
+    point within ~1 xatol."""
+    fin = np.isfinite(ref) & np.isfinite(dpd)
+    rel = np.zeros_like(ref)
+    rel[fin] = np.abs(dpd[fin] - ref[fin]) / np.abs(ref[fin])
+    return [{'distance': int(d), 'condition': int(c), 'rel': float(rel[d, c]),
+             'd_delta_over_xatol': float(abs(
+                 dpd[d, c] / (1 + dpd[d, c]) - ref[d, c] / (1 + ref[d, c]))
+                 / xatol)}
+            for d, c in zip(*np.nonzero(rel > bar))]
+
+
+def parity_vs_reference(ctx, o, n, bins, dmax, seed, dpd=None):
     """The metric's second half, max-|dq| vs reference: the timed step's own
     p-values (left in HBM by the last timed step), BH on the device, against
     the REFERENCE's end-to-end run on this same chromosome
@@ -607,6 +618,11 @@ def parity_vs_reference(ctx, o, n, bins, dmax, seed):
         'order': best[2], 'max_rel_dp': best[0], 'max_abs_dq': best[1],
         'note': 'the reference re-run with the pixels of every segment in '
                 'another order (cfg2_spread.npz, 6 orders incl. its own)'}
+    if dpd is not None:
+        # which segments carry a move beyond 1e-6 of the reference's own run
+        # (a move of the bench's p from 3e-7 to 6e-6 names its segment here)
+        out['segments_beyond_1e-6_vs_reference'] = segments_vs(
+            dpd, g['disp_per_dist'])
     out['reference_own_spread'] = {
         'max_rel_dp': max(rel(sp['p_sample__%d' % k], g['p'])
                           for k in sp['perms']),
@@ -1089,6 +1105,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
                 pass
 
         tl = table_lrt(torch, dev, ctx, D, C)
+        last = {}
 
         def step():
             if by_dist:
@@ -1101,6 +1118,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
                                             t_dist.data_ptr(), n, R, cond, C,
                                             D, reduce=reduce)
             tl(dpd, t_raw, t_f, t_dist, n, R, cond, o)
+            last['dpd'] = dpd
             return dpd
 
         elapsed, ev, per = timed_run(args, ctx, dist, dev, step)
@@ -1124,7 +1142,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
         out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
         if world == 1:
             out['parity_vs_reference'] = parity_vs_reference(
-                ctx, o, n, args.bins, args.dmax, rank)
+                ctx, o, n, args.bins, args.dmax, rank, last.get('dpd'))
         if cpu is not None:
             out['cpu_baseline'] = cpu[0]
             out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)

@@ -214,13 +214,16 @@ class CSR(object):
 _NPZ_SLACK = 4096
 
 
-def load_npz_csr(path):
+def load_npz_csr(path, alloc=None):
     """A scipy.sparse.save_npz CSR archive read by libh3d's reader
     (h3d_npz_csr_info / _read; the reference loads it with
     scipy.sparse.load_npz, analysis.py:94,100). Rows whose columns are not
     strictly increasing are canonicalised as scipy's sum_duplicates does.
     Raises H3DError for archives the reader does not take (other sparse
-    formats, unsupported dtypes); the caller decides whether to use scipy."""
+    formats, unsupported dtypes); the caller decides whether to use scipy.
+    ``alloc(nbytes)``: the uint8 buffers indices and data are inflated into
+    (default numpy; prepare_data passes pinned host memory, so the union's
+    uploads of them run at DMA speed)."""
     lib = load_library()
     if not hasattr(lib, 'h3d_npz_csr_read'):
         raise H3DError('libh3d.so predates h3d_npz_csr_read')
@@ -234,8 +237,9 @@ def load_npz_csr(path):
     if hasattr(lib, 'h3d_npz_csr_read_slack') and nnz.value > 0:
         # _NPZ_SLACK bytes ahead of indices / data: the members are inflated
         # in place, their .npy headers landing in the slack
-        ib = np.empty(_NPZ_SLACK + 4 * nnz.value, dtype=np.uint8)
-        db = np.empty(_NPZ_SLACK + 8 * nnz.value, dtype=np.uint8)
+        mk = alloc or (lambda k: np.empty(k, dtype=np.uint8))
+        ib = mk(_NPZ_SLACK + 4 * nnz.value)
+        db = mk(_NPZ_SLACK + 8 * nnz.value)
         indices = ib[_NPZ_SLACK:].view(np.int32)
         data = db[_NPZ_SLACK:].view(np.float64)
         _check(lib.h3d_npz_csr_read_slack(

@@ -34,7 +34,8 @@ from hic3defdr_amd.analysis.core import DispFn
 from hic3defdr_amd.analysis.d2h import to_host_async
 from hic3defdr_amd.util.classification import classify_clusters
 from hic3defdr_amd.util.cluster_table import ClusterTable
-from hic3defdr_amd.util.clusters import (load_clusters, load_cluster_list,
+from hic3defdr_amd.util.clusters import (load_cluster_list,
+                                         load_cluster_pixels,
                                          pixel_membership, save_clusters)
 from hic3defdr_amd.util.thresholding import threshold_clusters
 from hic3defdr_amd.util.printing import eprint
@@ -44,15 +45,35 @@ NATIVE_ESTIMATORS = ('qcml',)
 # H3D_RESIDENT=0: prepare_data does not keep the union in HBM (estimate_disp
 # and lrt then upload it from the outdir files, as a new process would)
 _KEEP_RESIDENT = os.environ.get('H3D_RESIDENT', '1') != '0'
+# chromosomes whose input files are read ahead of prepare_data's device work
+# (H3D_PREP_AHEAD; 1 = the next one only)
+_PREP_AHEAD = int(os.environ.get('H3D_PREP_AHEAD', '3'))
+_NPZ_PINNED = os.environ.get('H3D_NPZ_PINNED', '1') != '0'
+
+
+def _pinned_bytes(nbytes):
+    """A uint8 numpy array over pinned host memory (torch's caching host
+    allocator: a freed block serves the next chromosome's archives, so
+    the pinning is paid about once per run); pageable without torch or a
+    device."""
+    try:
+        import torch
+        return torch.empty(int(nbytes), dtype=torch.uint8,
+                           pin_memory=True).numpy()
+    except (ImportError, RuntimeError):   # no torch / no device to pin for
+        return np.empty(int(nbytes), dtype=np.uint8)
 
 
 def _canonical_csr(fname):
     """The replicate matrix as sorted, duplicate-free CSR rows (what the
     union kernels expect): libh3d's zlib reader for the CSR archives
-    save_npz writes, scipy for any other sparse format load_npz takes
-    (analysis.py:94,100)."""
+    save_npz writes -- inflated into pinned host memory (H3D_NPZ_PINNED=0:
+    pageable), so h3d_union_count's uploads are DMA copies instead of
+    staged pageable ones -- scipy for any other sparse format load_npz
+    takes (analysis.py:94,100)."""
     try:
-        return _native.load_npz_csr(fname)
+        return _native.load_npz_csr(fname, alloc=_pinned_bytes
+                                    if _NPZ_PINNED else None)
     except _native.H3DError:
         pass   # scipy reads it (or raises as the reference would)
     m = sparse.load_npz(fname).tocsr()
@@ -111,15 +132,21 @@ class AnalyzingHiC3DeFDR(object):
                 'norm=%r: the GPU path implements %s' % (norm, NATIVE_NORMS))
         if chrom is None:
             sh = self._shards()
-            # the next chromosome's files (NPZ inflate, bias, clusters) are
-            # read on threads while this one is prepared
-            with concurrent.futures.ThreadPoolExecutor(1) as pre:
-                nxt = pre.submit(self._prepare_inputs, sh.mine[0]) \
-                    if sh.mine else None
+            # the next chromosomes' files (NPZ inflate, bias, clusters) are
+            # read on threads while one is prepared: _PREP_AHEAD of them in
+            # flight (each inflating its replicates' archives on its own
+            # threads), so the device's per-chromosome work is not held up
+            # by one reader
+            ahead = max(1, _PREP_AHEAD)
+            with concurrent.futures.ThreadPoolExecutor(ahead) as pre:
+                futs = [pre.submit(self._prepare_inputs, c)
+                        for c in sh.mine[:ahead]]
                 for i, c in enumerate(sh.mine):
-                    inputs = nxt.result()
-                    nxt = pre.submit(self._prepare_inputs, sh.mine[i + 1]) \
-                        if i + 1 < len(sh.mine) else None
+                    inputs = futs[i].result()
+                    futs[i] = None
+                    if i + ahead < len(sh.mine):
+                        futs.append(pre.submit(self._prepare_inputs,
+                                               sh.mine[i + ahead]))
                     self._prepare_chrom(c, norm, n_bins, verbose, inputs)
             self._barrier(sh)
             return
@@ -135,7 +162,9 @@ class AnalyzingHiC3DeFDR(object):
             fut = [ex.submit(_canonical_csr, p.replace('<chrom>', chrom))
                    for p in self.raw_npz_patterns]
             bias = self.load_bias(chrom)
-            cl = [load_clusters(p.replace('<chrom>', chrom))
+            # the clusters' pixels as arrays (loop_idx needs only their
+            # union; parsed in C, not as Python sets of tuples)
+            cl = [load_cluster_pixels(p.replace('<chrom>', chrom))
                   for p in self.loop_patterns.values()] \
                 if self.loop_patterns else None
             mats = [f.result() for f in fut]
@@ -190,7 +219,7 @@ class AnalyzingHiC3DeFDR(object):
         if self.loop_patterns:
             eprint('  making loop_idx', skip=not verbose)
             loop_idx = pixel_membership(row[disp_idx], col[disp_idx], cl)
-            self.save_data(loop_idx, 'loop_idx', chrom)
+            self._save_npy(self._npy('loop_idx', chrom), loop_idx, owned=True)
         eprint('  saving data to disk', skip=not verbose)
         for name, a in (('row', row), ('col', col), ('raw', raw),
                         ('size_factors', size_factors), ('scaled', scaled),

@@ -4,6 +4,7 @@ contract between stages — ``<outdir>/<name>_<chrom>.npy`` per chromosome,
 import atexit
 import collections
 import concurrent.futures
+import ctypes
 import os
 import pickle
 import sys
@@ -87,11 +88,44 @@ class _Reaper(object):
         self._lock = threading.Lock()
         self._q = None
 
+    @staticmethod
+    def _release_pages(a):
+        """Returns the pages of numpy array ``a`` to the kernel with
+        madvise(MADV_DONTNEED) through ctypes -- which drops the GIL -- when
+        this thread holds the only reference to it and it owns its buffer:
+        the free() that follows then unmaps mostly released pages. numpy
+        frees a buffer while holding the GIL, so a large free on this thread
+        used to stall every Python thread (~36 ms per GB on the GPU box; the
+        main thread's GIL waits showed up in every call of prepare_data).
+        H3D_REAP_MADVISE=0 turns it off."""
+        if not _MADVISE or not isinstance(a, np.ndarray) or \
+                not a.flags.owndata or a.nbytes < _Reaper._MIN_BYTES:
+            return
+        # nobody else holds it: the references are _run's local, this
+        # frame's ``a`` and getrefcount's argument (a view's base or any
+        # other holder makes it more, and the pages stay)
+        if sys.getrefcount(a) > 3:
+            return
+        libc = _libc()
+        if libc is None:
+            return
+        page = 4096
+        addr = a.ctypes.data
+        lo = (addr + page - 1) // page * page
+        hi = (addr + a.nbytes) // page * page
+        if hi > lo:
+            libc.madvise(ctypes.c_void_p(lo), ctypes.c_size_t(hi - lo), 4)
+
     def _run(self):
         q = self._q
         while True:
             obj = q.get()
-            del obj
+            arrs = list(obj) if isinstance(obj, tuple) else [obj]
+            obj = None
+            while arrs:
+                a = arrs.pop()
+                self._release_pages(a)
+                a = None
 
     def drop(self, obj, nbytes):
         if nbytes < self._MIN_BYTES:
@@ -103,6 +137,24 @@ class _Reaper(object):
                 threading.Thread(target=self._run, name='h3d-reap',
                                  daemon=True).start()
         self._q.put(obj)
+
+
+_MADVISE = os.environ.get('H3D_REAP_MADVISE', '1') != '0' and \
+    sys.platform.startswith('linux')
+_LIBC = []
+
+
+def _libc():
+    if not _LIBC:
+        try:
+            lib = ctypes.CDLL(None, use_errno=True)
+            lib.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_int]
+            lib.madvise.restype = ctypes.c_int
+            _LIBC.append(lib)
+        except (OSError, AttributeError):
+            _LIBC.append(None)
+    return _LIBC[0]
 
 
 _REAPER = _Reaper()

@@ -17,6 +17,7 @@ Clustering itself is ``h3d_find_clusters`` in libh3d (host C++ restatement of
 the DirectedDisjointSet, clusters.py:15-97).
 """
 import json
+import re
 
 import numpy as np
 
@@ -156,6 +157,36 @@ def load_clusters(infile):
                 json.load(handle)]
 
 
+_PIXEL_TEXT = bytes.maketrans(b'[]', b'  ')
+_PAIR = rb'\[\d+,\d+\]'
+_CLUSTER = rb'\[(?:%s(?:,%s)*)?\]' % (_PAIR, _PAIR)
+_CLUSTER_FILE = re.compile(rb'\[(?:%s(?:,%s)*)?\]' % (_CLUSTER, _CLUSTER))
+
+
+def load_cluster_pixels(infile):
+    """Every pixel of a cluster JSON (reference clusters.py:176-193's file:
+    a list of clusters, each a list of [i, j]) as one (k, 2) int64 array,
+    parsed in C (numpy's text reader over the numbers) instead of as
+    Python sets of tuples -- what prepare_data's loop_idx needs (the union
+    of the clusters' pixels, analysis.py:117-125). Files that are not pure
+    nested lists of integer pairs go through json (load_clusters)."""
+    with open(infile, 'rb') as handle:
+        text = handle.read()
+    compact = text.translate(None, b' \t\r\n')
+    if _CLUSTER_FILE.fullmatch(compact):
+        body = compact.translate(_PIXEL_TEXT).replace(b',', b' ').strip()
+        if not body:
+            return np.zeros((0, 2), dtype=np.int64)
+        return np.fromstring(body.decode('ascii'), dtype=np.int64,
+                             sep=' ').reshape(-1, 2)
+    # anything else as the reference reads it; a pixel with a non-integer
+    # coordinate can match no (row, col) of the union
+    pix = np.array([p for cl in load_clusters(infile) for p in cl],
+                   dtype=np.float64).reshape(-1, 2)
+    pix = pix[np.all(pix == np.floor(pix), axis=1)]
+    return pix.astype(np.int64)
+
+
 def load_cluster_list(infile):
     """A cluster JSON as a ``ClusterList`` (file order kept)."""
     with open(infile, 'r') as handle:
@@ -191,11 +222,19 @@ def cluster_from_string(cluster_string):
 def pixel_membership(row, col, clusters_lists, n_bins=None):
     """Boolean vector: (row[k], col[k]) in the union of all clusters
     (reference ``analysis.py:117-125``, a Python set lookup per pixel),
-    vectorised with 64-bit pixel keys."""
-    pixels = set().union(*sum(clusters_lists, []))
-    if not pixels or len(row) == 0:
+    vectorised with 64-bit pixel keys. ``clusters_lists``: per condition a
+    list of pixel sets (load_clusters) or a (k, 2) pixel array
+    (load_cluster_pixels)."""
+    arrs = [c for c in clusters_lists if isinstance(c, np.ndarray)]
+    sets = [c for c in clusters_lists if not isinstance(c, np.ndarray)]
+    if sets:
+        pixels = set().union(*sum(sets, []))
+        if pixels:
+            arrs.append(np.array(sorted(pixels), dtype=np.int64))
+    arrs = [a.reshape(-1, 2) for a in arrs if len(a)]
+    if not arrs or len(row) == 0:
         return np.zeros(len(row), dtype=bool)
-    pix = np.array(sorted(pixels), dtype=np.int64)
+    pix = np.concatenate(arrs)
     return pixel_in(row, col, pix[:, 0], pix[:, 1])
 
 

@@ -12,6 +12,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
 s=$(find gpurun_out/${tag}_prof -name '*kernel_stats.csv' -print -quit)
 t=$(find gpurun_out/${tag}_prof -name '*kernel_trace.csv' -print -quit)
 cp "$s" gpurun_out/${tag}_kernel_stats.csv
+cp "$t" gpurun_out/${tag}_kernel_trace.csv
 python3 tools/trace_gaps.py "$t" 10 > gpurun_out/${tag}_gaps.txt
 python3 - "$tag" <<'PY'
 import csv, sys

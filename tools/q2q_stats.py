@@ -263,6 +263,39 @@ def wave_report(lib, raw, f, dist, dpd, cond, c, it_cost=18.0,
     tot = act_it + act_call + act_fit
     ideal = ideal_it + ideal_call + ideal_fit
     print('  modelled lane utilisation %.2f' % (ideal.sum() / tot.sum()))
+    # wave-local task sort: a wave's w x nr q2q tasks
+    # sorted by a key, then run as nr rounds of w lanes -- the q2q loop
+    # cost of each round is the max over its lanes per call position (CF and
+    # series paths paid separately), as above
+    tasks_it = itm.transpose(0, 2, 1, 3).reshape(nw, nr * w, 5)
+    tasks_pa = paths.transpose(0, 2, 1, 3).reshape(nw, nr * w, 5)
+    tasks_md = made.transpose(0, 2, 1, 3).reshape(nw, nr * w, 5)
+    cost = (np.where(tasks_pa == 0, cf_factor, 1.0) * tasks_it).sum(2)
+
+    def rounds(order):
+        it = np.take_along_axis(tasks_it, order[..., None], 1)
+        pa = np.take_along_axis(tasks_pa, order[..., None], 1)
+        md = np.take_along_axis(tasks_md, order[..., None], 1)
+        it = it.reshape(nw, nr, w, 5)
+        pa = pa.reshape(nw, nr, w, 5)
+        md = md.reshape(nw, nr, w, 5)
+        c_ = np.where(md & (pa == 0), it, 0)
+        s_ = np.where(md & (pa != 0), it, 0)
+        return ((cf_factor * c_.max(2) + s_.max(2)).sum(axis=(1, 2)) * it_cost
+                + md.any(2).sum(axis=(1, 2)) * call_cost)
+    keys = {
+        'oracle cost': cost,
+        'fwd path, fwd iters': tasks_pa[..., 0] * 1000 + tasks_it[..., 0],
+        'fwd path, inv path': tasks_pa[..., 0] * 10 + tasks_pa[..., 1],
+        'fwd path': tasks_pa[..., 0].astype(float),
+    }
+    base = act_it + act_call
+    for name, key in keys.items():
+        order = np.argsort(key, axis=1, kind='stable')
+        r = rounds(order)
+        print('   wave-local sort by %-22s: q2q loop+call cost %.0f vs %.0f '
+              '(%.1f%%)' % (name, r.mean(), base.mean(),
+                            100 * (r.mean() / base.mean() - 1)))
 
 
 if __name__ == '__main__':
