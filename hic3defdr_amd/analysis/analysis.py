@@ -46,8 +46,11 @@ NATIVE_ESTIMATORS = ('qcml',)
 # and lrt then upload it from the outdir files, as a new process would)
 _KEEP_RESIDENT = os.environ.get('H3D_RESIDENT', '1') != '0'
 # chromosomes whose input files are read ahead of prepare_data's device work
-# (H3D_PREP_AHEAD; 1 = the next one only)
-_PREP_AHEAD = int(os.environ.get('H3D_PREP_AHEAD', '3'))
+# (H3D_PREP_AHEAD; 1 = the next one only). Measured on the cfg3 genome
+# through run_to_qvalues (r06m, three interleaved runs each): 1.49-1.53 s at
+# 1, 1.55-1.60 s at 2, 1.57-1.82 s at 3 -- more readers in flight contend
+# with the outdir writers and the device thread for the host's cores
+_PREP_AHEAD = int(os.environ.get('H3D_PREP_AHEAD', '1'))
 _NPZ_PINNED = os.environ.get('H3D_NPZ_PINNED', '1') != '0'
 
 
@@ -134,9 +137,8 @@ class AnalyzingHiC3DeFDR(object):
             sh = self._shards()
             # the next chromosomes' files (NPZ inflate, bias, clusters) are
             # read on threads while one is prepared: _PREP_AHEAD of them in
-            # flight (each inflating its replicates' archives on its own
-            # threads), so the device's per-chromosome work is not held up
-            # by one reader
+            # flight, each inflating its replicates' archives on its own
+            # threads
             ahead = max(1, _PREP_AHEAD)
             with concurrent.futures.ThreadPoolExecutor(ahead) as pre:
                 futs = [pre.submit(self._prepare_inputs, c)
