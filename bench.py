@@ -1384,6 +1384,9 @@ def main():
                 cfg3['cpu'] = cpu_cfg3_run(cfg3['genome'], d3)
         if not args.no_e2e and not args.no_e2e_cfg3:
             cfg3['files'] = e2e_cfg3_files(d3)
+            # the genome's ~2 GB of input files reach the disk now, not in
+            # the page cache's background writeback during the timed legs
+            os.sync()
     import torch
     torch.cuda.set_device(local)
     peaks = None

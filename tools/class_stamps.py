@@ -41,6 +41,10 @@ def wrap(obj, name, label=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--runs', type=int, default=5)
+    ap.add_argument('--no-flush', action='store_true',
+                    help='no flush() between prepare_data and estimate_disp '
+                         '(prepare_data\'s background copies and writes still '
+                         'landing, as in run_to_qvalues)')
     args = ap.parse_args()
     import bench
     import torch  # noqa: F401
@@ -61,6 +65,7 @@ def main():
     wrap(torch, 'empty', 'torch.empty')
     wrap(numpy, 'empty', 'numpy.empty')
     wrap(d2h, '_pool', 'd2h._pool')
+    wrap(resident.Resident, 'lrt_buffers', 'Resident.lrt_buffers')
     wrap(torch.cuda, 'Event', 'torch.cuda.Event')
     for name in ('_save_npy', 'save_data', 'save_disp_fn', '_barrier',
                  '_shards', '_resident', '_cond_of_rep', '_lrt_run'):
@@ -75,7 +80,8 @@ def main():
                        design=h.design, outdir=out,
                        dist_thresh_max=h.dist_thresh_max)
         h2.prepare_data(verbose=False)
-        h2.flush()
+        if not args.no_flush:
+            h2.flush()
         row = {}
         for stage, fn in (('estimate_disp', h2.estimate_disp),
                           ('lrt', lambda: h2.lrt(verbose=False))):

@@ -1,9 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for rep in 1 2 3; do
-for v in "old H3D_PREP_AHEAD=1 H3D_NPZ_PINNED=0 H3D_REAP_MADVISE=0" "a1 H3D_PREP_AHEAD=1" "a2 H3D_PREP_AHEAD=2" "a3 H3D_PREP_AHEAD=3"; do
-  set -- $v; name=$1; shift
-  env "$@" timeout -k 10 300 python -u tools/run_e2e.py > gpurun_out/r06m_$name.json 2> gpurun_out/r06m_$name.err || exit 1
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['run_to_qvalues_s'],3), {k: round(v,3) for k,v in d['stages'].items()})" gpurun_out/r06m_$name.json $name
-done
-done
+timeout -k 10 900 python -u bench.py > gpurun_out/r06t_bench.json 2> gpurun_out/r06t_bench.err || exit 1
+python3 -c "import json,sys; d=json.loads(open('gpurun_out/r06t_bench.json').read().strip().splitlines()[-1]); e=d['e2e_run_to_qvalues']; print({k: round(v*1e3,2) for k,v in e.items() if isinstance(v,float)}, [round(x,3) for x in e['runs_total_s']]); print(d['value']/1e6, d['e2e_cfg3_run_to_qvalues']['total_s'])"

@@ -16,7 +16,8 @@ src = os.path.join(REPO, 'gpurun_out', 'pmc_%s_summary.json' % tag)
 kernels = json.load(open(src))
 out = {'bins': 20000, 'dmax': 250,
        'command': 'tools/pmc_passes.sh %s: rocprofv3 --pmc <pass> -- python3 '
-                  'bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e (one pass '
+                  'bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e '
+                  '--no-other-configs --no-peaks (one pass '
                   'each: SQ, F64, FETCH_SIZE, WRITE_SIZE)' % tag,
        'units': 'hbm_read_bytes_corrected = FETCH_SIZE KB x1024 x2 (gfx950 '
                 'correction); hbm_write_bytes = WRITE_SIZE KB x1024; SQ_* '
