@@ -53,6 +53,7 @@ events and from the committed rocprofv3 stats of the same command.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
 import shutil
@@ -1140,6 +1141,12 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
                 else 'per-pass NLL all-reduce over RCCL'), 'weak',
             peaks=peaks)
         out['gang_aborts'] = ctx.profile_read('gang_aborts')[1]
+        # the last step's disp_per_dist and p, hashed: A/B runs of kernel
+        # variants that must not move a bit compare this
+        torch.cuda.synchronize()
+        hsh = hashlib.sha256(np.ascontiguousarray(last['dpd']).tobytes())
+        hsh.update(o['p'].cpu().numpy().tobytes())
+        out['result_sha16'] = hsh.hexdigest()[:16]
         if world == 1:
             out['parity_vs_reference'] = parity_vs_reference(
                 ctx, o, n, args.bins, args.dmax, rank, last.get('dpd'))

@@ -285,7 +285,10 @@ class AnalyzingHiC3DeFDR(object):
         ctx = self._ctx()
         dev = torch.device('cuda', ctx.device)
         torch.cuda.set_device(dev)
-        torch.cuda.synchronize(dev)
+        # torch's stream only: a device-wide synchronize would also wait for
+        # the background copies of earlier stages' results (analysis/d2h.py,
+        # their own stream); libh3d's calls return with its stream drained
+        torch.cuda.current_stream(dev).synchronize()
         # a real stream shared by libh3d and the collective: torch's default
         # stream has handle 0, which h3d_set_stream reads as "the ctx's own
         # stream" -- the all-reduce would then race the kernels around it
@@ -352,12 +355,16 @@ class AnalyzingHiC3DeFDR(object):
                                                         D)
             t_dpd = torch.from_numpy(np.ascontiguousarray(disp_per_dist)).to(
                 res.dev)
-            torch.cuda.synchronize(res.dev)
+            torch.cuda.current_stream(res.dev).synchronize()
             ctx.disp_tables_dev(t_dpd.data_ptr(), D, C, t_tab.data_ptr(),
                                 weighted=weighted_lowess, frac=frac,
                                 auto_frac_factor=auto_frac_factor)
         else:
-            torch.cuda.synchronize(res.dev)
+            # torch's stream only (the allocations above): a device-wide
+            # synchronize also waited for prepare_data's background result
+            # copies (d2h.py, their own stream) -- up to ~30 ms of cfg2's
+            # estimate_disp through the class
+            torch.cuda.current_stream(res.dev).synchronize()
             disp_per_dist = ctx.estimate_disp_dev(
                 t_raw.data_ptr() if n else None, t_f.data_ptr() if n else None,
                 t_dist.data_ptr() if n else None, n, R, cond, C, D,

@@ -238,6 +238,19 @@ void launch_brent(h3d_ctx* ctx, const double* pd, int64_t n, const int64_t* seg_
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBrentBlock), lds_px ? lds_px * 8 * M : 0,
                      ctx->stream, pd, n, seg_start, S, C, rep_idx, n_rep, st, seg_flags,
                      result, queue, ctx->work_count, lds_px, gate_meta, live_min, gang_abort);
+#ifdef H3D_BRENT_CLOCK
+  unsigned long long clk[38];
+  (void)hipMemcpyFromSymbolAsync(clk, HIP_SYMBOL(g_brent_clk), sizeof(clk), 0,
+                                 hipMemcpyDeviceToHost, ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream);
+  fprintf(stderr, "[brent_clk] sum %llu bar1 %llu step %llu bar2 %llu stage %llu total %llu\n",
+          clk[0], clk[1], clk[2], clk[3], clk[4], clk[5]);
+  fprintf(stderr, "[brent_clk_wave] sum");
+  for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", clk[6 + i]);
+  fprintf(stderr, " bar1");
+  for (int i = 0; i < 16; ++i) fprintf(stderr, " %llu", clk[22 + i]);
+  fprintf(stderr, "\n");
+#endif
 }
 
 // the gang variant (k_brent_gang): every live segment's search over the

@@ -861,22 +861,54 @@ static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int 
 // __launch_bounds__(512, 4)). MODE 2: every argument >= kNllLargeR
 // (nll_pixel_large); 1: >= kNllMidR (nll_pixel_mid); 0: nll_pixel.
 // (nll_pixel_large).
-template <int M, int kBlockT, int MODE>
+#ifndef H3D_BRENT_PAIR2
+#define H3D_BRENT_PAIR2 2
+#endif
+// pixels per trip of brent_segment_sum
+template <int M>
+constexpr int kPair2() {
+  return M <= 2 ? H3D_BRENT_PAIR2 : M <= 4 ? 2 : 1;
+}
+#ifndef H3D_BRENT_PRIO
+#define H3D_BRENT_PRIO 1
+#endif
+// The wave's issue priority by its progress through the segment (kPrio,
+// k_brent): 3 at the start of an evaluation, one lower at each quarter of
+// its trips. The SIMD otherwise prefers the older of its four waves
+// throughout, so the waves finished one after another and the last ran
+// alone (H3D_BRENT_CLOCK, r06v: the four age ranks' sums took 1.26 / 1.75 /
+// 2.33 / 2.89 G cycles); a wave ahead now yields to the ones behind it.
+// Arbitration only: the terms and their order are unchanged.
+__device__ __forceinline__ void brent_prio(int& cur, int trip, int ntr) {
+  const int lv = __builtin_amdgcn_readfirstlane(
+      3 - min(3, (4 * trip) / max(ntr, 1)));
+  if (lv == cur) return;
+  cur = lv;
+  if (lv == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (lv == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else if (lv == 0)
+    __builtin_amdgcn_s_setprio(0);
+}
+
+template <int M, int kBlockT, int MODE, bool kPrio = false>
 __device__ __forceinline__ double brent_segment_sum(
     const double* s_pd, int64_t lds_px, const double* __restrict__ pd, int64_t n,
     const int* ri, int nr, int64_t b, int64_t el, int64_t e, const NllConst& kc,
     const LogTab* s_tab) {
   double acc = 0.0;
-#ifndef H3D_BRENT_PAIR2
-#define H3D_BRENT_PAIR2 2
-#endif
-  constexpr int kPair = M <= 2 ? H3D_BRENT_PAIR2 : M <= 4 ? 2 : 1;
+  [[maybe_unused]] int trip = 0, lv = 3;
+  [[maybe_unused]] const int ntr = (int)((e - b + kPair2<M>() * kBlockT - 1) / (kPair2<M>() * kBlockT));
+  if constexpr (kPrio) __builtin_amdgcn_s_setprio(3);
+  constexpr int kPair = kPair2<M>();
   auto term = [&](const double* v) {
     if constexpr (MODE == 2) return nll_pixel_large<M>(v, nr, kc, s_tab);
     else if constexpr (MODE == 1) return nll_pixel_mid<M>(v, nr, kc, s_tab);
     else return nll_pixel<M>(v, nr, kc, s_tab);
   };
   for (int64_t i = threadIdx.x; i < el - b; i += kPair * kBlockT) {
+    if constexpr (kPrio) brent_prio(lv, trip++, ntr);
     double v[kPair][M];
     bool on[kPair];
 #pragma unroll
@@ -894,6 +926,7 @@ __device__ __forceinline__ double brent_segment_sum(
       if (on[q]) acc += t[q];
   }
   for (int64_t px = el + threadIdx.x; px < e; px += kPair * kBlockT) {
+    if constexpr (kPrio) brent_prio(lv, trip++, ntr);
     double v[kPair][M];
     bool on[kPair];
 #pragma unroll
@@ -918,6 +951,18 @@ __device__ __forceinline__ double brent_segment_sum(
 // every evaluation reads them from there and streams only the rest -- the
 // segment used to be re-read from beyond L2 on every evaluation (PMC: 859 MB
 // fetched per launch for 74 MB of pseudodata, waves waiting half the time).
+#ifdef H3D_BRENT_CLOCK
+// measurement build only: per-wave shader-clock totals of k_brent's phases
+// [sum, barrier after the sum, seg_step (wave 0), barrier after the step,
+// head staging, whole kernel], printed by launch_brent
+__device__ unsigned long long g_brent_clk[6 + 2 * 16];
+#define H3D_BCLK(v) const long long v = clock64()
+#define H3D_BADD(i, d) clk[i] += (unsigned long long)(d)
+#else
+#define H3D_BCLK(v)
+#define H3D_BADD(i, d)
+#endif
+
 template <int M>
 __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     const double* __restrict__ pd, int64_t n,
@@ -946,6 +991,10 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
   __shared__ LogTab s_tab[kLogTabLen];
   for (int t = threadIdx.x; t < kLogTabLen; t += kBrentBlock) s_tab[t] = kLogTab[t];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef H3D_BRENT_CLOCK
+  unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};
+  H3D_BCLK(k_t0);
+#endif
   while (true) {
     __syncthreads();  // s_next / s_st reuse
     if (threadIdx.x == 0) s_next = atomicAdd(queue, 1);
@@ -953,6 +1002,7 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     const int s = s_next;
     if (s >= S) break;
     if (st[s].phase != kEqualize) continue;  // done, or nothing to search
+    H3D_BCLK(c_stage0);
     if (threadIdx.x == 0) {
       s_st = st[s];
       s_st.flags |= seg_flags[s];
@@ -971,21 +1021,27 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
     }
     int evals = 0;
     __syncthreads();
+    H3D_BCLK(c_stage1);
+    H3D_BADD(4, c_stage1 - c_stage0);
     while (true) {
+      H3D_BCLK(c0);
       const NllConst kc = s_st.k;
       // every lgamma argument >= r: at r >= kNllLargeR / kNllMidR the short
       // paths (nll_pixel_large / _mid), the same for every thread of the
       // segment
+      constexpr bool kPr = H3D_BRENT_PRIO != 0;
       const double acc = (kc.r >= kNllLargeR)
-          ? brent_segment_sum<M, kBrentBlock, 2>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
+          ? brent_segment_sum<M, kBrentBlock, 2, kPr>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
           : (kc.r >= kNllMidR)
-          ? brent_segment_sum<M, kBrentBlock, 1>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
-          : brent_segment_sum<M, kBrentBlock, 0>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab);
+          ? brent_segment_sum<M, kBrentBlock, 1, kPr>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab)
+          : brent_segment_sum<M, kBrentBlock, 0, kPr>(s_pd, lds_px, pd, n, ri, nr, b, el, e, kc, s_tab);
       double wacc = acc;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) wacc += __shfl_xor(wacc, off, 64);
       if (lane == 0) wpart[wid] = wacc;
+      H3D_BCLK(c1);
       __syncthreads();
+      H3D_BCLK(c2);
       if (threadIdx.x == 0) {
         double total = 0.0;
 #pragma unroll
@@ -993,8 +1049,14 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
         seg_step_ool(&s_st, total, nr);
         s_more = (s_st.phase == kNll) ? 1 : 0;
       }
+      H3D_BCLK(c3);
       ++evals;
       __syncthreads();  // s_st / s_more / wpart
+      H3D_BCLK(c4);
+      H3D_BADD(0, c1 - c0);
+      H3D_BADD(1, c2 - c1);
+      H3D_BADD(2, c3 - c2);
+      H3D_BADD(3, c4 - c3);
       if (!s_more) break;
     }
     if (threadIdx.x == 0) {
@@ -1004,6 +1066,18 @@ __global__ __launch_bounds__(brent_block<M>(), M >= 16 ? 2 : 4) void k_brent(
       atomicAdd(&work_count[1], (unsigned long long)(e - b) * nr * evals);
     }
   }
+#ifdef H3D_BRENT_CLOCK
+  H3D_BCLK(k_t1);
+  clk[5] = (unsigned long long)(k_t1 - k_t0);
+  if (lane == 0) {
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_brent_clk[i], clk[i]);
+    // per wave of the workgroup: its sum and first-barrier cycles
+    if (wid < 16) {
+      atomicAdd(&g_brent_clk[6 + wid], clk[0]);
+      atomicAdd(&g_brent_clk[22 + wid], clk[1]);
+    }
+  }
+#endif
 }
 
 // ---- gang Brent: a segment's search over several co-resident workgroups ----

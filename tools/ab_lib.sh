@@ -48,7 +48,7 @@ for sp in $specs; do
     env $(echo "$envs" | tr ',' ' ') $libenv timeout -k 10 400 python3 -u $cmd \
       > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err
   fi
-  python3 -c "import json; d=json.loads(open('gpurun_out/ab_$name.json').read().strip().splitlines()[-1]); k=d['kernels_ms_per_step']; print('$name', round(d['value']/1e6,1), round(d['ms_per_step'],3), {a: round(b,3) for a, b in k.items() if a != 'note'})" | tee -a gpurun_out/ab_summary.txt
+  python3 -c "import json; d=json.loads(open('gpurun_out/ab_$name.json').read().strip().splitlines()[-1]); k=d['kernels_ms_per_step']; print('$name', round(d['value']/1e6,1), round(d['ms_per_step'],3), d.get('result_sha16'), {a: round(b,3) for a, b in k.items() if a != 'note'})" | tee -a gpurun_out/ab_summary.txt
 done
 done
 if [ "$tests" = 1 ]; then
