@@ -1396,6 +1396,9 @@ def main():
             os.sync()
     import torch
     torch.cuda.set_device(local)
+    # the process's threads on its GPU's NUMA node (H3D_NUMA_BIND=0: not)
+    from hic3defdr_amd import numa
+    numa_bind = numa.maybe_bind(local, default=True)
     peaks = None
     if rank == 0 and not args.no_peaks:
         peaks = measured_peaks(local)
@@ -1417,6 +1420,7 @@ def main():
         else:
             out = run_cfg3(args, world, rank, local, dist, ctx, dev, peaks)
         if rank == 0:
+            out['numa_bind'] = numa_bind
             print(json.dumps(out), flush=True)
     finally:
         if dist:

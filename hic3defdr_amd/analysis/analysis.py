@@ -29,7 +29,7 @@ import os
 import numpy as np
 import scipy.sparse as sparse
 
-from hic3defdr_amd import _native, parallel
+from hic3defdr_amd import _native, numa, parallel
 from hic3defdr_amd.analysis.core import DispFn
 from hic3defdr_amd.analysis.d2h import to_host_async
 from hic3defdr_amd.util.classification import classify_clusters
@@ -52,6 +52,7 @@ _KEEP_RESIDENT = os.environ.get('H3D_RESIDENT', '1') != '0'
 # with the outdir writers and the device thread for the host's cores
 _PREP_AHEAD = int(os.environ.get('H3D_PREP_AHEAD', '1'))
 _NPZ_PINNED = os.environ.get('H3D_NPZ_PINNED', '1') != '0'
+_NUMA_DONE = []
 
 
 def _pinned_bytes(nbytes):
@@ -97,7 +98,12 @@ def _pixel_factors(bias, row, col, size_factors):
 class AnalyzingHiC3DeFDR(object):
 
     def _ctx(self):
-        return _native.context(parallel.device_for_rank())
+        dev = parallel.device_for_rank()
+        if not _NUMA_DONE:
+            # H3D_NUMA_BIND=1: this process's threads on its GPU's NUMA node
+            # (numa.py), once, before the stages start their threads
+            _NUMA_DONE.append(numa.maybe_bind(dev))
+        return _native.context(dev)
 
     def _shards(self):
         """This rank's chromosomes (all of them without a process group);
