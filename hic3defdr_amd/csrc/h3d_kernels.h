@@ -481,6 +481,9 @@ __global__ __launch_bounds__(kBlock, W) void k_disp_work(
   __syncthreads();
   int64_t t = t0 + (int64_t)blockIdx.x * kWv + (threadIdx.x >> 6);
   if (t >= tdyn) t = take();
+  // (taking the wave's next task at the top of this one, so the dequeue's
+  // round trip runs under this task's arithmetic, measured slower: equalize
+  // 2.57 -> 2.66 ms per cfg2 step, r06z)
   for (; t < t1; t = (t + wt < tdyn) ? t + wt : take()) {
     const int w = (int)(t / kWv);
     const int q = (int)(t - (int64_t)w * kWv);
@@ -1191,6 +1194,7 @@ __global__ __launch_bounds__(kGangThreads) void k_brent_gang(
     while (true) {
       const NllConst kc = s_st.k;
       // the slice (no LDS head), two pixels per trip for M <= 4, as k_brent
+      // (the progress priority of k_brent measured neutral here, r06z)
       double acc = (kc.r >= kNllLargeR)
           ? brent_segment_sum<M, kGangThreads, 2>(nullptr, 0, pd, n, ri, nr, sb, sb, se, kc, s_tab)
           : (kc.r >= kNllMidR)
