@@ -35,13 +35,13 @@ EXPORTS = [
     'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
     'h3d_disp_pixels_dev', 'h3d_table_gather_dev', 'h3d_disp_seg_stats',
     'h3d_scale_disp_dev', 'h3d_npz_backend', 'h3d_npz_csr_read_slack',
-    'h3d_pixel_f_dev',
+    'h3d_pixel_f_dev', 'h3d_read_text_column',
 ]
 
 
 # entry points a library built from an older tree may lack; callers check
 OPTIONAL = ('h3d_find_clusters_ordered', 'h3d_npz_backend',
-            'h3d_npz_csr_read_slack',
+            'h3d_npz_csr_read_slack', 'h3d_read_text_column',
             'h3d_disp_tables', 'h3d_npz_csr_info', 'h3d_npz_csr_read',
             'h3d_disp_tables_dev', 'h3d_disp_tables_wait', 'h3d_lrt_dev_tab',
             'h3d_estimate_disp_dev')
@@ -156,6 +156,7 @@ def load_library(path=None):
                                      _I, _P, _P, _P, _P, _P]),
             'h3d_npz_csr_info': (_I, [ctypes.c_char_p, _P, _P, _P]),
             'h3d_npz_backend': (_I, []),
+            'h3d_read_text_column': (_I, [ctypes.c_char_p, _P, _I64, _P]),
             'h3d_npz_csr_read_slack': (_I, [ctypes.c_char_p, _I64, _I64, _P,
                                             _P, _P, _I64, _P]),
             'h3d_npz_csr_read': (_I, [ctypes.c_char_p, _I64, _I64, _P, _P, _P,
@@ -209,6 +210,30 @@ class CSR(object):
     def __init__(self, indptr, indices, data, shape):
         self.indptr, self.indices, self.data = indptr, indices, data
         self.shape = shape
+
+
+def read_text_column(path):
+    """A one-column text file (a replicate's bias vector) as np.loadtxt
+    reads it, parsed by libh3d (h3d_read_text_column) without holding the
+    GIL -- prepare_data's reader thread parses the next chromosome's bias
+    files while the main thread drives the device, and np.loadtxt held the
+    GIL for all of it. None when libh3d does not take the file (anything but
+    one decimal number per line, or an older library): the caller reads it
+    with np.loadtxt."""
+    try:
+        lib = load_library()
+        size = os.path.getsize(path)
+    except (H3DError, OSError):
+        return None
+    if not hasattr(lib, 'h3d_read_text_column'):
+        return None
+    cap = size // 2 + 1          # a value takes at least a digit and a newline
+    out = np.empty(cap)
+    n = ctypes.c_int64(0)
+    if lib.h3d_read_text_column(os.fsencode(path), _ptr(out), cap,
+                                ctypes.byref(n)) != 0:
+        return None
+    return out[:n.value]
 
 
 _NPZ_SLACK = 4096

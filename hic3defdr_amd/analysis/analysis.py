@@ -32,6 +32,7 @@ import scipy.sparse as sparse
 from hic3defdr_amd import _native, numa, parallel
 from hic3defdr_amd.analysis.core import DispFn
 from hic3defdr_amd.analysis.d2h import to_host_async
+from hic3defdr_amd.analysis.resident import bias_stamps
 from hic3defdr_amd.util.classification import classify_clusters
 from hic3defdr_amd.util.cluster_table import ClusterTable
 from hic3defdr_amd.util.clusters import (load_cluster_list,
@@ -162,13 +163,18 @@ class AnalyzingHiC3DeFDR(object):
                             self._prepare_inputs(chrom))
 
     def _prepare_inputs(self, chrom):
-        """One chromosome's input files: bias (load_bias), the replicates'
-        canonical CSR matrices (their NPZ archives inflated concurrently:
-        zlib inflate and crc32 release the GIL) and the loop clusters."""
+        """One chromosome's input files: bias (load_bias, and the bias
+        files' stamps for the resident session), the replicates' canonical
+        CSR matrices (their NPZ archives inflated concurrently: zlib inflate
+        and crc32 release the GIL) and the loop clusters."""
         with concurrent.futures.ThreadPoolExecutor(
                 min(8, len(self.raw_npz_patterns))) as ex:
             fut = [ex.submit(_canonical_csr, p.replace('<chrom>', chrom))
                    for p in self.raw_npz_patterns]
+            # stamped before reading: a file replaced while it is read shows
+            # as changed to the session's validity checks
+            stamps = bias_stamps(self.bias_patterns, chrom) \
+                if _KEEP_RESIDENT else None
             bias = self.load_bias(chrom)
             # the clusters' pixels as arrays (loop_idx needs only their
             # union; parsed in C, not as Python sets of tuples)
@@ -176,13 +182,13 @@ class AnalyzingHiC3DeFDR(object):
                   for p in self.loop_patterns.values()] \
                 if self.loop_patterns else None
             mats = [f.result() for f in fut]
-        return bias, mats, cl
+        return bias, mats, cl, stamps
 
     def _prepare_chrom(self, chrom, norm, n_bins, verbose, inputs):
         """prepare_data of one chromosome (analysis.py:28-133) from its
         input files (_prepare_inputs)."""
         eprint('preparing data for chrom %s' % chrom, skip=not verbose)
-        bias, mats, cl = inputs
+        bias, mats, cl, stamps = inputs
         ctx = self._ctx()
         res = self._resident() if _KEEP_RESIDENT else None
         holder = {}
@@ -235,7 +241,7 @@ class AnalyzingHiC3DeFDR(object):
             self._save_npy(self._npy(name, chrom), a, owned=True,
                            ready=ready.get(name))
         if res is not None and 'sf' in holder:
-            res.keep(chrom, holder, disp_idx, bias)
+            res.keep(chrom, holder, disp_idx, bias, bias_stamps=stamps)
 
     # ------------------------------------------------------------------
     def _f_and_dist(self, chroms=None):

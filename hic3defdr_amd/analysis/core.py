@@ -22,6 +22,14 @@ def _write_npy(fname, data, ready=None):
     return (st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns)
 
 
+def _load_column(fname):
+    """np.loadtxt of a one-column text file, parsed by libh3d when it takes
+    the file (_native.read_text_column: the same values, no GIL held)."""
+    from hic3defdr_amd import _native
+    col = _native.read_text_column(fname)
+    return np.loadtxt(fname) if col is None else col
+
+
 def _write_bytes(fname, blob):
     with open(fname, 'wb') as fh:
         fh.write(blob)
@@ -235,7 +243,7 @@ class CoreHiC3DeFDR(object):
     def load_bias(self, chrom):
         """Reference ``core.py:35-60``: (n_bins, R); bins failing
         ``bias_thresh`` in any replicate are zeroed."""
-        bias = np.column_stack([np.loadtxt(p.replace('<chrom>', chrom))
+        bias = np.column_stack([_load_column(p.replace('<chrom>', chrom))
                                 for p in self.bias_patterns])
         lo, hi = self.bias_thresh, 1. / self.bias_thresh
         bias[((bias < lo) | (bias > hi)).any(axis=1)] = 0

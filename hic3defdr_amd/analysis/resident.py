@@ -45,6 +45,12 @@ def _stamp(fname):
     return (st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns)
 
 
+def bias_stamps(bias_patterns, chrom):
+    """{bias file: ('disk', stamp)} of one chromosome's bias files."""
+    return {f: ('disk', _stamp(f)) for f in
+            (p.replace('<chrom>', chrom) for p in bias_patterns)}
+
+
 class ChromDev(object):
     """One chromosome's union pixels on the device."""
 
@@ -92,8 +98,7 @@ class Resident(object):
         return ('disk', _stamp(fname))
 
     def _bias_stamps(self, chrom):
-        return {f: ('disk', _stamp(f)) for f in
-                (p.replace('<chrom>', chrom) for p in self.h.bias_patterns)}
+        return bias_stamps(self.h.bias_patterns, chrom)
 
     # -- prepare_data ----------------------------------------------------
     def union_alloc(self, holder):
@@ -172,8 +177,10 @@ class Resident(object):
         scaled, ready = to_host_async(t_scaled)
         return scaled, ready, disp_idx
 
-    def keep(self, chrom, holder, disp_idx, bias):
-        """Registers a prepared chromosome (its stage files just queued)."""
+    def keep(self, chrom, holder, disp_idx, bias, bias_stamps=None):
+        """Registers a prepared chromosome (its stage files just queued).
+        ``bias_stamps``: the bias files' stamps taken where they were read
+        (bias_stamps(); prepare_data's reader thread), else taken here."""
         torch = self.torch
         n = int(holder['row'].shape[0])
         t_di = holder.get('di')
@@ -182,7 +189,8 @@ class Resident(object):
                 disp_idx, dtype=np.uint8)).to(self.dev)
         files = {self.h._npy(s, chrom): ('ours', self.h.write_generation(
             self.h._npy(s, chrom))) for s in self.STAGES}
-        files.update(self._bias_stamps(chrom))
+        files.update(bias_stamps if bias_stamps is not None
+                     else self._bias_stamps(chrom))
         self.chroms[chrom] = ChromDev(
             holder['row'], holder['col'], holder['raw'], holder['sf'],
             holder['sf'].dim() == 1, t_di, int(np.count_nonzero(disp_idx)),

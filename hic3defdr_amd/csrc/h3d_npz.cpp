@@ -16,6 +16,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -441,6 +442,59 @@ int h3d_npz_csr_read_slack(const char* path, int64_t n_rows, int64_t nnz, int64_
   } catch (const std::exception& e) {
     return fail(H3D_ENOMEM, "npz: %s", e.what());
   }
+}
+
+// One number per line, as np.loadtxt reads a one-column file (load_bias,
+// core.py:35-60, the replicates' bias vectors): blank lines and '#' comments
+// skipped, each value by strtod (correctly rounded, as numpy's own parser).
+// Anything else -- two tokens on a line, a hex float, trailing characters --
+// is H3D_EINPUT, and the caller reads the file with np.loadtxt instead.
+// Host only, no GIL: prepare_data's reader thread calls it while the main
+// thread drives the device.
+int h3d_read_text_column(const char* path, double* out, int64_t cap, int64_t* n) {
+  if (!path || !n || (cap > 0 && !out)) return fail(H3D_EARG, "null argument");
+  *n = 0;
+  FILE* fh = std::fopen(path, "rb");
+  if (!fh) return fail(H3D_EARG, "text column: cannot open %s", path);
+  std::vector<char> text;
+  try {
+    char buf[1 << 16];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof(buf), fh)) > 0) text.insert(text.end(), buf, buf + got);
+  } catch (const std::exception& e) {
+    std::fclose(fh);
+    return fail(H3D_ENOMEM, "text column: %s", e.what());
+  }
+  std::fclose(fh);
+  text.push_back('\0');
+  const char* q = text.data();
+  const char* end = q + text.size() - 1;
+  int64_t k = 0;
+  while (q < end) {
+    const char* eol = static_cast<const char*>(std::memchr(q, '\n', end - q));
+    if (!eol) eol = end;
+    const char* hash = static_cast<const char*>(std::memchr(q, '#', eol - q));
+    const char* le = hash ? hash : eol;
+    const char* a = q;
+    while (a < le && std::isspace((unsigned char)*a)) ++a;
+    const char* b = le;
+    while (b > a && std::isspace((unsigned char)b[-1])) --b;
+    if (a < b) {
+      for (const char* c = a; c < b; ++c)
+        if (std::isspace((unsigned char)*c) || *c == 'x' || *c == 'X')
+          return fail(H3D_EINPUT, "text column: %s line %lld is not one number", path,
+                      (long long)(k + 1));
+      char* stop = nullptr;
+      const double v = std::strtod(a, &stop);
+      if (stop != b) return fail(H3D_EINPUT, "text column: %s: not a number", path);
+      if (k >= cap) return fail(H3D_EARG, "text column: %s has more than %lld values", path,
+                                (long long)cap);
+      out[k++] = v;
+    }
+    q = eol + 1;
+  }
+  *n = k;
+  return 0;
 }
 
 }  // extern "C"

@@ -114,6 +114,14 @@ int h3d_npz_csr_read_slack(const char* path, int64_t n_rows, int64_t nnz,
                            int64_t slack, int* canonical);
 /* 1 when the reader inflates through libdeflate, 0 through zlib. */
 int h3d_npz_backend(void);
+/* A one-column text file as np.loadtxt reads it -- load_bias's bias vectors
+ * (core.py:35-60: np.loadtxt per replicate file): one number per line, blank
+ * lines and '#' comments skipped, values by strtod (correctly rounded, as
+ * numpy's parser). *n = the values written to out (capacity cap). H3D_EINPUT
+ * for any line that is not exactly one decimal number (the caller then reads
+ * the file with np.loadtxt and its errors); H3D_EARG for a missing file or
+ * more than cap values. Host only. */
+int h3d_read_text_column(const char* path, double* out, int64_t cap, int64_t* n);
 
 /* Union pixel set of R upper-triangular CSR replicate matrices restricted to
  * 0 <= col-row <= dist_max and to bins whose bias is non-zero in every
