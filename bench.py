@@ -684,7 +684,8 @@ def e2e_cfg3(base, kw, write_s, runs=2):
     first = _e2e_once(h, base, 'first', drop=True)
     per = [_e2e_once(h, base, k, drop=True) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k != 'note'}
+           if k not in ('note', 'gc_collections')}
+    out['gc_collections'] = [r['gc_collections'] for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
     out['write_genome_s'] = write_s
@@ -703,7 +704,8 @@ def e2e_wall(h, tmp, runs=3):
     first = _e2e_once(h, tmp, runs)
     per = [_e2e_once(h, tmp, k) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k != 'note'}
+           if k not in ('note', 'gc_collections')}
+    out['gc_collections'] = [r['gc_collections'] for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
     out['note'] = per[0]['note'] + '; per-stage medians of %d runs after ' \
@@ -712,30 +714,66 @@ def e2e_wall(h, tmp, runs=3):
     return out
 
 
+class _GcClock(object):
+    """Wall time the interpreter's garbage collector spent between start()
+    and stop() (gc.callbacks), and its collections of each generation."""
+
+    def __init__(self):
+        self.t0, self.total, self.counts = None, 0.0, [0, 0, 0]
+
+    def __call__(self, phase, info):
+        if phase == 'start':
+            self.t0 = time.perf_counter()
+        elif self.t0 is not None:
+            self.total += time.perf_counter() - self.t0
+            self.counts[info.get('generation', 0)] += 1
+            self.t0 = None
+
+    def start(self):
+        import gc
+        gc.callbacks.append(self)
+        return self
+
+    def stop(self):
+        import gc
+        gc.callbacks.remove(self)
+        return self
+
+
 def _e2e_once(h, tmp, k, drop=False):
     from hic3defdr_amd import HiC3DeFDR
     out = os.path.join(tmp, 'out_e2e_%s' % k)
     os.makedirs(out, exist_ok=True)
+    gcc = _GcClock().start()
     h2 = HiC3DeFDR(raw_npz_patterns=h.raw_npz_patterns,
                    bias_patterns=h.bias_patterns, chroms=h.chroms,
                    design=h.design, outdir=out,
                    dist_thresh_max=h.dist_thresh_max,
                    loop_patterns=h.loop_patterns, res=h.res)
     t = [time.perf_counter()]
+    g = [0.0]
     h2.prepare_data(verbose=False)
     t.append(time.perf_counter())
+    g.append(gcc.total)
     h2.estimate_disp()
     t.append(time.perf_counter())
+    g.append(gcc.total)
     h2.lrt(verbose=False)
     t.append(time.perf_counter())
+    g.append(gcc.total)
     h2.bh()
     t.append(time.perf_counter())
+    g.append(gcc.total)
     h2.flush()
     t.append(time.perf_counter())
+    g.append(gcc.total)
+    gcc.stop()
     del h2
     if drop:
         shutil.rmtree(out, ignore_errors=True)
-    return {'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
+    return {'gc_s': gcc.total, 'gc_collections': gcc.counts,
+            'gc_estimate_disp_s': g[2] - g[1],
+            'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
             'estimate_disp_s': t[2] - t[1], 'lrt_s': t[3] - t[2],
             'bh_s': t[4] - t[3], 'outdir_flush_s': t[5] - t[4],
             'estimate_disp_plus_lrt_s': t[3] - t[1],
