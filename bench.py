@@ -684,7 +684,7 @@ def e2e_cfg3(base, kw, write_s, runs=2):
     first = _e2e_once(h, base, 'first', drop=True)
     per = [_e2e_once(h, base, k, drop=True) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k not in ('note', 'gc_collections')}
+           if k not in ('note', 'gc_collections') and per[0][k] is not None}
     out['gc_collections'] = [r['gc_collections'] for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
@@ -704,7 +704,7 @@ def e2e_wall(h, tmp, runs=3):
     first = _e2e_once(h, tmp, runs)
     per = [_e2e_once(h, tmp, k) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k not in ('note', 'gc_collections')}
+           if k not in ('note', 'gc_collections') and per[0][k] is not None}
     out['gc_collections'] = [r['gc_collections'] for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
@@ -740,11 +740,25 @@ class _GcClock(object):
         return self
 
 
+def _cgroup_throttled_s():
+    """Seconds this cgroup's threads have been held by its CPU quota
+    (cgroup v2 cpu.stat throttled_usec), or None."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as fh:
+            for ln in fh:
+                if ln.startswith('throttled_usec'):
+                    return int(ln.split()[1]) * 1e-6
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
 def _e2e_once(h, tmp, k, drop=False):
     from hic3defdr_amd import HiC3DeFDR
     out = os.path.join(tmp, 'out_e2e_%s' % k)
     os.makedirs(out, exist_ok=True)
     gcc = _GcClock().start()
+    thr0 = _cgroup_throttled_s()
     h2 = HiC3DeFDR(raw_npz_patterns=h.raw_npz_patterns,
                    bias_patterns=h.bias_patterns, chroms=h.chroms,
                    design=h.design, outdir=out,
@@ -768,11 +782,14 @@ def _e2e_once(h, tmp, k, drop=False):
     t.append(time.perf_counter())
     g.append(gcc.total)
     gcc.stop()
+    thr1 = _cgroup_throttled_s()
     del h2
     if drop:
         shutil.rmtree(out, ignore_errors=True)
     return {'gc_s': gcc.total, 'gc_collections': gcc.counts,
             'gc_estimate_disp_s': g[2] - g[1],
+            'cgroup_throttled_s': (thr1 - thr0) if thr0 is not None and
+            thr1 is not None else None,
             'total_s': t[-1] - t[0], 'prepare_data_s': t[1] - t[0],
             'estimate_disp_s': t[2] - t[1], 'lrt_s': t[3] - t[2],
             'bh_s': t[4] - t[3], 'outdir_flush_s': t[5] - t[4],
@@ -1192,6 +1209,12 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
             out['cpu_baseline'] = cpu[0]
             out['parity_sample'] = sample_parity(ctx, cpu[1], args.dmax)
         if world == 1 and not args.no_e2e:
+            # the bench's own objects (CPU legs, fixtures) out of the
+            # collector's young generations: their collections are not the
+            # product's (cfg3 e2e: 60 ms of gc per run before, r06ae)
+            import gc
+            gc.collect()
+            gc.freeze()
             out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
             if cfg3 and cfg3.get('files'):
                 base, kw, w_s = cfg3['files']

@@ -850,7 +850,9 @@ static __global__ __launch_bounds__(1024) void k_seg_update(
 // 4.6 vs 6.4 ms per step -- the per-task acquire and arrival traffic cost
 // more than the tail the static grid leaves idle.
 // seg_step out of line for k_brent: run by one thread once per evaluation,
-// its registers stay out of the NLL loop's budget. (nll_const's two lgammas
+// its registers stay out of the NLL loop's budget (the state stays in LDS:
+// stepping a register copy measured slower, Brent 1.97-2.00 -> 2.01-2.02 ms
+// per cfg2 step, r06ae). (nll_const's two lgammas
 // of the next trial point on two lanes at once measured within noise:
 // Brent 2.00-2.01 -> 1.98-2.00 ms per cfg2 step, r06aa -- not kept.)
 static __device__ __noinline__ void seg_step_ool(SegState* s, double total, int n_reps) {

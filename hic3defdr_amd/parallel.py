@@ -450,7 +450,10 @@ def chrom_sizes(bias_patterns, chroms):
     out = {}
     for c in chroms:
         with open(bias_patterns[0].replace('<chrom>', c), 'rb') as fh:
-            out[c] = sum(1 for _ in fh)
+            data = fh.read()
+        # the file's lines (a last one without its newline counts)
+        out[c] = data.count(b'\n') + (1 if data and not
+                                       data.endswith(b'\n') else 0)
     return out
 
 
