@@ -35,7 +35,7 @@ EXPORTS = [
     'h3d_bh_finish_dev', 'h3d_union_fill_dev', 'h3d_size_factors_dev',
     'h3d_disp_pixels_dev', 'h3d_table_gather_dev', 'h3d_disp_seg_stats',
     'h3d_scale_disp_dev', 'h3d_npz_backend', 'h3d_npz_csr_read_slack',
-    'h3d_pixel_f_dev', 'h3d_read_text_column',
+    'h3d_pixel_f_dev', 'h3d_read_text_column', 'h3d_set_qcml_tol',
 ]
 
 
@@ -99,6 +99,7 @@ def load_library(path=None):
             'h3d_close': (None, [_P]),
             'h3d_last_error': (ctypes.c_char_p, []),
             'h3d_set_stream': (_I, [_P, _P]),
+            'h3d_set_qcml_tol': (_I, [_P, _D]),
             'h3d_union_count': (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
             'h3d_union_fill': (_I, [_P, _P, _P, _P, _P, _I64]),
             'h3d_union_fill_dev': (_I, [_P, _P, _P, _P, _P, _I64, _P, _P, _P,
@@ -313,6 +314,12 @@ class Context(object):
     def set_stream(self, stream_handle):
         _check(self.lib.h3d_set_stream(self.handle, stream_handle),
                'h3d_set_stream')
+
+    def set_qcml_tol(self, tol):
+        """qcml's convergence tolerance for this ctx's later estimate_disp
+        calls (h3d_set_qcml_tol; dispersion.py:10's tol, default 1e-4)."""
+        _check(self.lib.h3d_set_qcml_tol(self.handle, float(tol)),
+               'h3d_set_qcml_tol')
 
     # -- prepare_data -------------------------------------------------------
     def sparse_union(self, csrs, bias, dist_max, device_alloc=None,

@@ -521,6 +521,13 @@ int h3d_set_stream(h3d_ctx* ctx, void* stream) {
   return 0;
 }
 
+int h3d_set_qcml_tol(h3d_ctx* ctx, double tol) {
+  if (!ctx) return fail(H3D_EARG, "null ctx");
+  if (!(tol >= 0.0) || !(tol < INFINITY)) return fail(H3D_EARG, "qcml tol %g", tol);
+  ctx->qcml_tol = tol;
+  return 0;
+}
+
 int h3d_profile_enable(h3d_ctx* ctx, int on) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   prof_collect(ctx);
@@ -872,7 +879,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       HIP_TRY(hipMemcpyAsync(cnt.data(), d_cnt, S * 8, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
     }
-    for (int sg = 0; sg < S; ++sg) seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C]);
+    for (int sg = 0; sg < S; ++sg)
+      seg_init(&st[sg], (long long)cnt[sg], nrep[sg % C], ctx->qcml_tol);
     for (int d = 0; d < D; ++d)
       for (int c = 0; c < C; ++c) lpx[d * C + c] = seg_start[d + 1] - seg_start[d];
   }
@@ -975,7 +983,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     hipLaunchKernelGGL(k_disp_tables, dim3(1), dim3(1024), 0, s, d_seg0, D, C, n, d_nrep,
                        d_cs, d_cl, d_cd, d_scb, d_sce, d_st, d_lpx, d_bad,
                        dual ? gang.P : (int64_t)1, dual ? gang.task_seg : nullptr,
-                       dual ? gang.task_g : nullptr);
+                       dual ? gang.task_g : nullptr, ctx->qcml_tol);
     dbg_launch("k_disp_tables");
   }
   stamp("tables uploaded");

@@ -129,6 +129,7 @@ struct h3d_ctx {
   // LDS too, r03am: 64 / 96 / 128 KB 2.62-2.66 ms of Brent per cfg2 step,
   // 80 / 112 / 144 KB 2.73-2.80 (the replicate rows' LDS stride), 0 KB 2.67
   int brent_lds_kb = 128;
+  double qcml_tol = 1e-4;  // h3d_set_qcml_tol (qcml's tol, dispersion.py:10)
   // gang Brent slice (pixels; 0 = sized from the call, gang_setup_dev)
   int gang_px = 0;
   // k_brent_gang tag epoch (tags carry it, so they need no clearing between

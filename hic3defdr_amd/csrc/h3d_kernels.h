@@ -337,7 +337,7 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
     int32_t* __restrict__ cl, int32_t* __restrict__ cd, int32_t* __restrict__ scb,
     int32_t* __restrict__ sce, SegState* __restrict__ st, int64_t* __restrict__ lpx,
     int* __restrict__ bad, int64_t gang_P, int32_t* __restrict__ task_seg,
-    int32_t* __restrict__ task_g) {
+    int32_t* __restrict__ task_g, double tol) {
   __shared__ int s_wsum[16], s_tsum[16];
   __shared__ int s_carry, s_tcarry;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -393,7 +393,7 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
         cd[b0 + j] = d;
       }
       for (int c = 0; c < C; ++c) {
-        seg_init(&st[d * C + c], (long long)len, n_rep[c]);
+        seg_init(&st[d * C + c], (long long)len, n_rep[c], tol);
         lpx[d * C + c] = len;
       }
     }

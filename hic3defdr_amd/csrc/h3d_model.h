@@ -595,6 +595,7 @@ constexpr double kBrentA = 1e-4;
 constexpr double kBrentB = 100. / (100 + 1);
 constexpr double kXatol = 1e-5;
 constexpr int kMaxFun = 500;
+constexpr double kQcmlTol = 1e-4;  // qcml's default tol (dispersion.py:10)
 
 struct SegState {
   int phase;
@@ -608,6 +609,7 @@ struct SegState {
   double result;  // final qcml dispersion (NaN for an empty segment)
   NllConst k;     // nll constants at x for n = replicates of the condition
   double a, b, xf, fx, nfc, fnfc, fulc, ffulc, e, rat, xm, tol1, tol2, fu;
+  double tol;     // qcml's convergence tolerance on |disp - new disp|
 };
 
 H3D_HD double brent_sqrt_eps() { return sqrt(2.2e-16); }
@@ -616,7 +618,8 @@ H3D_HD double brent_x0() {
   return kBrentA + brent_golden() * (kBrentB - kBrentA);
 }
 
-H3D_HD void seg_init(SegState* s, long long n_px, int n_reps) {
+H3D_HD void seg_init(SegState* s, long long n_px, int n_reps, double tol = kQcmlTol) {
+  s->tol = tol;
   s->flags = 0;
   s->num = 0;
   s->qiter = 0;
@@ -741,12 +744,12 @@ H3D_HD void seg_step(SegState* s, double total, int n_reps) {
   const double delta = fabs(s->disp - new_disp);
   s->disp = new_disp;
   s->qiter += 1;
-  if (delta > 1e-4 && s->qiter < 1000 && !(s->flags & kFlagBrentFail)) {
+  if (delta > s->tol && s->qiter < 1000 && !(s->flags & kFlagBrentFail)) {
     s->phase = kEqualize;
     s->x = brent_x0();
     s->k = nll_const(s->x, n_reps);
   } else {
-    if (s->qiter >= 1000 && delta > 1e-4) s->flags |= kFlagQcmlGuard;
+    if (s->qiter >= 1000 && delta > s->tol) s->flags |= kFlagQcmlGuard;
     s->phase = kDone;
     s->result = s->disp;
   }

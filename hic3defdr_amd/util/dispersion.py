@@ -18,13 +18,27 @@ import numpy as np
 from hic3defdr_amd import _native
 
 
+def _tol_scope(ctx, tol):
+    """The ctx's qcml tolerance set to ``tol`` for one call, restored to
+    the estimate_disp default (1e-4) after it."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def scope():
+        ctx.set_qcml_tol(tol)
+        try:
+            yield
+        finally:
+            ctx.set_qcml_tol(1e-4)
+    return scope()
+
+
 def qcml(data, f=None, max_iter=10, tol=1e-4):
     """dispersion.py:10-43. ``max_iter`` is accepted and, as in the
-    reference (whose loop counter is never incremented), has no effect; the
-    convergence tolerance is the reference's default 1e-4."""
+    reference (whose loop counter is never incremented), has no effect;
+    ``tol``: iterate while |disp - new disp| > tol (the device state
+    machine's own tolerance, h3d_set_qcml_tol)."""
     data = np.asarray(data)
-    if tol != 1e-4:
-        raise NotImplementedError('the device qcml converges at tol=1e-4')
     if data.ndim != 2:
         raise ValueError('data must be (pixels, replicates)')
     if data.size and not np.all(data == np.floor(data)):
@@ -32,8 +46,10 @@ def qcml(data, f=None, max_iter=10, tol=1e-4):
     n, r = data.shape
     f = np.ones((n, r)) if f is None else np.broadcast_to(f, (n, r))
     ctx = _native.context()
-    out = ctx.disp_per_dist(data.astype(np.int64), f, np.zeros(n, np.int32),
-                            np.zeros(r, np.int32), 1, 1)
+    with _tol_scope(ctx, tol):
+        out = ctx.disp_per_dist(data.astype(np.int64), f,
+                                np.zeros(n, np.int32), np.zeros(r, np.int32),
+                                1, 1)
     return float(out[0, 0])
 
 
@@ -51,8 +67,6 @@ def qcml_batch(segments, max_iter=10, tol=1e-4):
     condition) (analysis.py:198-246 -> dispersion.py:10-43): a caller
     patching that loop gathers its segments first and makes this one call
     instead of several hundred single-segment driver runs."""
-    if tol != 1e-4:
-        raise NotImplementedError('the device qcml converges at tol=1e-4')
     out = [np.nan] * len(segments)
     by_r = {}
     for i, (data, f) in enumerate(segments):
@@ -71,8 +85,10 @@ def qcml_batch(segments, max_iter=10, tol=1e-4):
         ff = np.concatenate([f for _, _, f in group]).astype(np.float64)
         dist = np.concatenate([np.full(len(d), j, np.int32)
                                for j, (_, d, _) in enumerate(group)])
-        res = ctx.disp_per_dist(raw.reshape(-1, r), ff.reshape(-1, r), dist,
-                                np.zeros(r, np.int32), 1, len(group))
+        with _tol_scope(ctx, tol):
+            res = ctx.disp_per_dist(raw.reshape(-1, r), ff.reshape(-1, r),
+                                    dist, np.zeros(r, np.int32), 1,
+                                    len(group))
         for j, (i, _, _) in enumerate(group):
             out[i] = float(res[j, 0])
     return out

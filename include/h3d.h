@@ -86,6 +86,11 @@ void h3d_close(h3d_ctx* ctx);
 const char* h3d_last_error(void);
 /* stream the ctx launches on (hipStream_t); NULL = the ctx's own stream */
 int h3d_set_stream(h3d_ctx* ctx, void* stream);
+/* qcml's convergence tolerance for the ctx's later estimate_disp calls
+ * (util/dispersion.py:10-43 qcml(..., tol=1e-4): iterate while
+ * |disp - new disp| > tol); default 1e-4, the value the reference's
+ * estimate_disp uses. H3D_EARG for a negative or non-finite tol. */
+int h3d_set_qcml_tol(h3d_ctx* ctx, double tol);
 
 /* ---- prepare_data ------------------------------------------------------ */
 

@@ -73,3 +73,24 @@ def test_qcml_batch_equals_per_segment_calls():
     print('qcml: %d segments, %.2f ms per single-segment call, %.2f ms for '
           'the batch' % (len(segs), (t1 - t0) / len(segs) * 1e3,
                          (t2 - t1) * 1e3))
+
+
+def test_qcml_tol_vs_oracle():
+    """qcml(tol=...) (dispersion.py:10-43: iterate while |disp - new disp|
+    > tol) on the device state machine against the oracle's qcml at the
+    same tol; the ctx's tolerance is back at the default afterwards (the
+    next default call equals the reference's value)."""
+    import oracle
+    from hic3defdr_amd.util import dispersion
+    g = golden('unit_nb.npz')
+    for s in range(int(g['n_segs'])):
+        data, f = g['seg%d_data' % s], g['seg%d_f' % s]
+        for tol in (1e-2, 1e-3, 1e-6):
+            got = dispersion.qcml(data, f=f, tol=tol)
+            want = oracle.qcml(data.astype(float), f=f, tol=tol)
+            assert rel_err(got, want) < 1e-6, (s, tol, got, want)
+        got = dispersion.qcml_batch([(data, f)], tol=1e-2)[0]
+        assert rel_err(got, oracle.qcml(data.astype(float), f=f, tol=1e-2)) < 1e-6
+        assert rel_err(dispersion.qcml(data, f=f), g['seg%d_qcml' % s]) < 1e-6
+    with pytest.raises(Exception):
+        dispersion.qcml(g['seg0_data'], f=g['seg0_f'], tol=-1.0)
