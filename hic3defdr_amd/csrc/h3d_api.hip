@@ -704,7 +704,12 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
                              hipMemcpyHostToDevice, s));
       const bool k32 = end_bit <= 16;
       // 32-bit keys: (distance, 8-bit min / max count codes), sorted over
-      // end_bit + 16 bits (cfg2: 24 bits, three radix passes)
+      // end_bit + 16 bits (cfg2: 24 bits, three radix passes). (A stable
+      // scatter into distance buckets, then each bucket sorted in LDS, gave
+      // the same order but measured slower: prep 0.55 -> 1.19 ms per cfg2
+      // step, r06aj / r06ak -- the scatter's 4-byte writes to ~250 buckets
+      // are uncoalesced (195 us) and the LDS bitonic sorts LDS-bound (555
+      // us); the radix passes stage their scatter through LDS.)
       const int cbits = k32 ? 16 : 64 - end_bit;
       const int sort_bits = k32 ? end_bit + 16 : 64;
       // every condition of <= 2 replicates: one key pass for all of them,
