@@ -395,8 +395,8 @@ int gang_setup_dev(h3d_ctx* ctx, int64_t n, int D, int C, GangTables* g) {
   g->abort = (int*)scratch(ctx, "gang_abort", 4);
   if (!g->task_seg || !g->task_g || !g->part || !g->tag || !g->abort)
     return fail(H3D_ENOMEM, "gang tables");
-  HIP_TRY(hipMemsetAsync(g->task_seg, 0xff, (size_t)g->T * 4, ctx->stream));
-  HIP_TRY(hipMemsetAsync(g->abort, 0, 4, ctx->stream));
+  // (task_seg's tail and abort are set by k_disp_tables, which fills the
+  // table)
   g->timeout = gang_timeout(ctx);
   return 0;
 }
@@ -957,7 +957,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       !d_st || !d_lpx || !d_list || !d_meta || !d_slb || !d_sle || !d_partial ||
       !d_total || !d_flags || !d_res)
     return fail(H3D_ENOMEM, "disp scratch");
-  HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));
+  if (!dev_tables) HIP_TRY(hipMemsetAsync(d_flags, 0, S * 4, s));  // else k_disp_tables
   int* d_bad = (int*)scratch(ctx, "dist_bad", 4);
   if (!d_bad) return fail(H3D_ENOMEM, "dist_bad");
   // (an M = 6 instantiation for cfg4's R_c = 6 measured equal to M = 8:
@@ -988,7 +988,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
     hipLaunchKernelGGL(k_disp_tables, dim3(1), dim3(1024), 0, s, d_seg0, D, C, n, d_nrep,
                        d_cs, d_cl, d_cd, d_scb, d_sce, d_st, d_lpx, d_bad,
                        dual ? gang.P : (int64_t)1, dual ? gang.task_seg : nullptr,
-                       dual ? gang.task_g : nullptr, ctx->qcml_tol);
+                       dual ? gang.task_g : nullptr, ctx->qcml_tol, dual ? gang.T : 0,
+                       d_flags, dual ? gang.abort : nullptr);
     dbg_launch("k_disp_tables");
   }
   stamp("tables uploaded");

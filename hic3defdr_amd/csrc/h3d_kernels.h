@@ -337,7 +337,8 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
     int32_t* __restrict__ cl, int32_t* __restrict__ cd, int32_t* __restrict__ scb,
     int32_t* __restrict__ sce, SegState* __restrict__ st, int64_t* __restrict__ lpx,
     int* __restrict__ bad, int64_t gang_P, int32_t* __restrict__ task_seg,
-    int32_t* __restrict__ task_g, double tol) {
+    int32_t* __restrict__ task_g, double tol, int task_len, int* __restrict__ seg_flags,
+    int* __restrict__ gang_abort) {
   __shared__ int s_wsum[16], s_tsum[16];
   __shared__ int s_carry, s_tcarry;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -345,7 +346,11 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
     s_carry = 0;
     s_tcarry = 0;
     *bad = (seg[0] != 0 || seg[D] != n) ? 1 : 0;
+    if (gang_abort) *gang_abort = 0;
   }
+  // (the segment flags zeroed here rather than by a fill launch each call)
+  if (seg_flags)
+    for (int k = threadIdx.x; k < D * C; k += 1024) seg_flags[k] = 0;
   __syncthreads();
   for (int base = 0; base < D; base += 1024) {
     const int d = base + threadIdx.x;
@@ -404,6 +409,9 @@ static __global__ __launch_bounds__(1024) void k_disp_tables(
     }
     __syncthreads();
   }
+  // the task table's unused tail (k_brent_gang skips -1 entries)
+  if (task_seg)
+    for (int t = s_tcarry + threadIdx.x; t < task_len; t += 1024) task_seg[t] = -1;
 }
 
 // Work item w of the active list: item = chunk * C + c.
