@@ -887,6 +887,9 @@ constexpr int kPair2() {
 #ifndef H3D_BRENT_PRIO
 #define H3D_BRENT_PRIO 1
 #endif
+#ifndef H3D_BRENT_PRIO_DIV
+#define H3D_BRENT_PRIO_DIV 4  // priority steps per evaluation (levels 3..0)
+#endif
 // The wave's issue priority by its progress through the segment (kPrio,
 // k_brent): 3 at the start of an evaluation, one lower at each quarter of
 // its trips. The SIMD otherwise prefers the older of its four waves
@@ -899,7 +902,7 @@ constexpr int kPair2() {
 // (r06y) -- the quarters stay.
 __device__ __forceinline__ void brent_prio(int& cur, int trip, int ntr) {
   const int lv = __builtin_amdgcn_readfirstlane(
-      3 - min(3, (4 * trip) / max(ntr, 1)));
+      3 - min(3, (H3D_BRENT_PRIO_DIV * trip) / max(ntr, 1)));
   if (lv == cur) return;
   cur = lv;
   if (lv == 2)
