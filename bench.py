@@ -684,8 +684,12 @@ def e2e_cfg3(base, kw, write_s, runs=2):
     first = _e2e_once(h, base, 'first', drop=True)
     per = [_e2e_once(h, base, k, drop=True) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k not in ('note', 'gc_collections') and per[0][k] is not None}
+           if k not in ('note', 'gc_collections', 'estimate_disp_stamps_ms')
+           and per[0][k] is not None}
     out['gc_collections'] = [r['gc_collections'] for r in per]
+    if 'estimate_disp_stamps_ms' in per[0]:
+        out['estimate_disp_stamps_ms'] = [r['estimate_disp_stamps_ms']
+                                          for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
     out['write_genome_s'] = write_s
@@ -704,8 +708,12 @@ def e2e_wall(h, tmp, runs=3):
     first = _e2e_once(h, tmp, runs)
     per = [_e2e_once(h, tmp, k) for k in range(runs)]
     out = {k: statistics.median(r[k] for r in per) for k in per[0]
-           if k not in ('note', 'gc_collections') and per[0][k] is not None}
+           if k not in ('note', 'gc_collections', 'estimate_disp_stamps_ms')
+           and per[0][k] is not None}
     out['gc_collections'] = [r['gc_collections'] for r in per]
+    if 'estimate_disp_stamps_ms' in per[0]:
+        out['estimate_disp_stamps_ms'] = [r['estimate_disp_stamps_ms']
+                                          for r in per]
     out['runs_total_s'] = [r['total_s'] for r in per]
     out['first_run'] = {k: v for k, v in first.items() if k != 'note'}
     out['note'] = per[0]['note'] + '; per-stage medians of %d runs after ' \
@@ -738,6 +746,39 @@ class _GcClock(object):
         import gc
         gc.callbacks.remove(self)
         return self
+
+
+_E2E_STAMPS = {}
+
+
+def _e2e_stamps_on():
+    """H3D_E2E_STAMPS=1: the e2e legs time the host calls inside
+    estimate_disp (tools/class_stamps.py's wrappers), per run."""
+    if os.environ.get('H3D_E2E_STAMPS') != '1' or 'acc' in _E2E_STAMPS:
+        return
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(
+        __file__)), 'tools'))
+    import class_stamps as cs
+    import numpy
+    import torch
+    from hic3defdr_amd import _native
+    from hic3defdr_amd.analysis import analysis, core, resident
+    ctx = _native.context(0)
+    for name in ('estimate_disp_dev', 'table_gather_dev'):
+        cs.wrap(ctx, name, 'ctx.' + name)
+    for name in ('disp_pixels', 'start_session', 'lrt_buffers'):
+        cs.wrap(resident.Resident, name, 'Resident.' + name)
+    cs.wrap(analysis, 'to_host_async', 'to_host_async')
+    cs.wrap(torch, 'empty', 'torch.empty')
+    cs.wrap(numpy, 'empty', 'numpy.empty')
+    cs.wrap(torch.cuda.Stream, 'synchronize', 'Stream.synchronize')
+    cs.wrap(torch.Tensor, 'cpu', 'Tensor.cpu')
+    for name in ('_save_npy', 'save_data', 'save_disp_fn', '_barrier',
+                 '_shards', '_resident', '_cond_of_rep', '_ctx'):
+        cls = core.CoreHiC3DeFDR if hasattr(core.CoreHiC3DeFDR, name) \
+            else analysis.AnalyzingHiC3DeFDR
+        cs.wrap(cls, name, 'HiC3DeFDR.' + name)
+    _E2E_STAMPS['acc'] = cs.ACC
 
 
 def _cgroup_throttled_s():
@@ -775,9 +816,14 @@ def _e2e_once(h, tmp, k, drop=False):
     h2.prepare_data(verbose=False)
     t.append(time.perf_counter())
     g.append(gcc.total)
+    stamps = _E2E_STAMPS.get('acc')
+    if stamps is not None:
+        stamps.clear()
     h2.estimate_disp()
     t.append(time.perf_counter())
     g.append(gcc.total)
+    est_stamps = {k: round(v * 1e3, 3) for k, v in stamps.items()} \
+        if stamps is not None else None
     h2.lrt(verbose=False)
     t.append(time.perf_counter())
     g.append(gcc.total)
@@ -792,7 +838,8 @@ def _e2e_once(h, tmp, k, drop=False):
     del h2
     if drop:
         shutil.rmtree(out, ignore_errors=True)
-    return {'gc_s': gcc.total, 'gc_collections': gcc.counts,
+    out_stamps = {'estimate_disp_stamps_ms': est_stamps} if est_stamps else {}
+    return {**out_stamps, 'gc_s': gcc.total, 'gc_collections': gcc.counts,
             'gc_estimate_disp_s': g[2] - g[1],
             'cgroup_throttled_s': (thr1 - thr0) if thr0 is not None and
             thr1 is not None else None,
@@ -1221,6 +1268,7 @@ def run_cfg2(args, world, rank, local, dist, ctx, dev, cpu, cfg3=None,
             import gc
             gc.collect()
             gc.freeze()
+            _e2e_stamps_on()
             out['e2e_run_to_qvalues'] = e2e_wall(h, tmp)
             if cfg3 and cfg3.get('files'):
                 base, kw, w_s = cfg3['files']

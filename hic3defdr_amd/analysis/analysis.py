@@ -31,7 +31,7 @@ import scipy.sparse as sparse
 
 from hic3defdr_amd import _native, numa, parallel
 from hic3defdr_amd.analysis.core import DispFn
-from hic3defdr_amd.analysis.d2h import to_host_async
+from hic3defdr_amd.analysis.d2h import small_to_host, to_host_async
 from hic3defdr_amd.analysis.resident import bias_stamps
 from hic3defdr_amd.util.classification import classify_clusters
 from hic3defdr_amd.util.cluster_table import ClusterTable
@@ -390,7 +390,7 @@ class AnalyzingHiC3DeFDR(object):
         # (table_gather_dev returns with the ctx stream drained); the per-pixel
         # disp goes to the outdir by a copy into pageable host memory on a
         # background thread (analysis/d2h.py; pinning measured slower there)
-        tables = t_tab.cpu().numpy()
+        tables = small_to_host(t_tab)
         disp, disp_ready = to_host_async(t_disp)
         del t_disp
         if sh.rank == 0:

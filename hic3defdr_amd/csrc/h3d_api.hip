@@ -58,6 +58,48 @@ void* scratch_keep(h3d_ctx* ctx, const char* slot, size_t bytes, size_t keep) {
   return p;
 }
 
+int h2d_pinned(h3d_ctx* ctx, void* d_dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return 0;
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (!ctx->bounce_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->bounce_ev, hipEventDisableTiming));
+  // the buffer is rewritten only after every earlier copy out of it has
+  // read it: wrap-around, growth and a change of stream wait on the last one
+  const bool wrap = ctx->bounce_off + need > ctx->bounce_cap;
+  if ((wrap || (ctx->bounce_stream && ctx->bounce_stream != s)) && ctx->bounce_stream) {
+    HIP_TRY(hipEventSynchronize(ctx->bounce_ev));
+    ctx->bounce_off = 0;
+    ctx->bounce_stream = nullptr;
+  }
+  if (need > ctx->bounce_cap) {
+    if (ctx->bounce) (void)hipHostFree(ctx->bounce);
+    ctx->bounce = nullptr;
+    ctx->bounce_cap = 0;
+    const size_t cap = std::max<size_t>(need, (size_t)1 << 20);
+    HIP_TRY(hipHostMalloc(&ctx->bounce, cap, hipHostMallocDefault));
+    ctx->bounce_cap = cap;
+    ctx->bounce_off = 0;
+  }
+  char* b = (char*)ctx->bounce + ctx->bounce_off;
+  std::memcpy(b, src, bytes);
+  HIP_TRY(hipMemcpyAsync(d_dst, b, bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(ctx->bounce_ev, s));
+  ctx->bounce_stream = s;
+  ctx->bounce_off += need;
+  return 0;
+}
+
+void* pinned_rd(h3d_ctx* ctx, size_t bytes) {
+  if (bytes > ctx->land_cap) {
+    if (ctx->land) (void)hipHostFree(ctx->land);
+    ctx->land = nullptr;
+    ctx->land_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 4096);
+    if (hipHostMalloc(&ctx->land, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    ctx->land_cap = cap;
+  }
+  return ctx->land;
+}
+
 hipEvent_t ev_get(h3d_ctx* ctx) {
   if (!ctx->event_pool.empty()) {
     hipEvent_t e = ctx->event_pool.back();
@@ -511,6 +553,9 @@ void h3d_close(h3d_ctx* ctx) {
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_stage_done) (void)hipEventDestroy(ctx->h_stage_done);
+  if (ctx->bounce) (void)hipHostFree(ctx->bounce);
+  if (ctx->bounce_ev) (void)hipEventDestroy(ctx->bounce_ev);
+  if (ctx->land) (void)hipHostFree(ctx->land);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -700,8 +745,8 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
       idx_out = (int32_t*)scratch(ctx, "idx_out_c", (size_t)n * 4);
       int32_t* d_reps = (int32_t*)scratch(ctx, "sort_reps", (size_t)C * kMaxReps * 4);
       if (!idx_out || !d_reps) return fail(H3D_ENOMEM, "sort buffers");
-      HIP_TRY(hipMemcpyAsync(d_reps, rep_idx.data(), (size_t)C * kMaxReps * 4,
-                             hipMemcpyHostToDevice, s));
+      if (int rc = h2d_pinned(ctx, d_reps, rep_idx.data(), (size_t)C * kMaxReps * 4, s))
+        return rc;
       const bool k32 = end_bit <= 16;
       // 32-bit keys: (distance, 8-bit min / max count codes), sorted over
       // end_bit + 16 bits (cfg2: 24 bits, three radix passes). (A stable
@@ -721,7 +766,7 @@ int disp_per_dist_core(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
         d_nrep = (int32_t*)scratch(ctx, "sort_nrep", (size_t)C * 4);
         packed = (CondPack2*)scratch(ctx, "cond_pack2", (size_t)C * n * sizeof(CondPack2));
         if (!d_nrep || !packed) return fail(H3D_ENOMEM, "packed gather rows");
-        HIP_TRY(hipMemcpyAsync(d_nrep, nrep.data(), (size_t)C * 4, hipMemcpyHostToDevice, s));
+        if (int rc = h2d_pinned(ctx, d_nrep, nrep.data(), (size_t)C * 4, s)) return rc;
       }
       void* keys = scratch(ctx, "dkeys", (pack ? (size_t)C : 1) * n * (k32 ? 4 : 8));
       void* keys_s = scratch(ctx, "dkeys_s", n * (k32 ? 4 : 8));

@@ -96,6 +96,17 @@ struct h3d_ctx {
   // before rewriting (or freeing) the buffer, whichever way the last call
   // returned
   hipEvent_t h_stage_done = nullptr;
+  // pinned bounce buffers for the small host<->device copies of the host
+  // entry points (h2d_pinned / pinned_rd): a copy from or to pageable memory
+  // is staged by the HIP runtime behind every other pageable copy in flight
+  // -- e.g. the class's background result copies -- and a 4-byte flag read
+  // waited tens of ms behind them (r06an)
+  void* bounce = nullptr;
+  size_t bounce_cap = 0, bounce_off = 0;
+  hipEvent_t bounce_ev = nullptr;
+  hipStream_t bounce_stream = nullptr;
+  void* land = nullptr;
+  size_t land_cap = 0;
   // tuning knobs (env at h3d_open): H3D_DISP_W = min waves/SIMD of the
   // disp_work register budget (1, 2, 3, 4); H3D_DISP_SORT = 0 (distance) or
   // 1 (distance, total count)
@@ -161,6 +172,13 @@ void* scratch(h3d_ctx* ctx, const char* slot, size_t bytes);
 // copy; growth at least doubles the capacity)
 void* scratch_keep(h3d_ctx* ctx, const char* slot, size_t bytes, size_t keep);
 hipEvent_t ev_get(h3d_ctx* ctx);
+// host -> device copy of `bytes` through the ctx's pinned bounce buffer,
+// stream-ordered on s (the source may be reused at once)
+int h2d_pinned(h3d_ctx* ctx, void* d_dst, const void* src, size_t bytes, hipStream_t s);
+// a pinned landing zone of >= bytes for device -> host copies (grow-only;
+// one user at a time: the caller synchronises before reading it and before
+// its next call), nullptr on failure
+void* pinned_rd(h3d_ctx* ctx, size_t bytes);
 // folds the recorded event pairs into ctx->stats (synchronises the stream)
 void prof_collect(h3d_ctx* ctx);
 // grid of a grid-stride elementwise kernel over n items

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "h3d.h"
@@ -78,7 +79,7 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
   if (!d_tab || !d_cond || !d_fl) return fail(H3D_ENOMEM, "lrt scratch");
   if (!table_on_dev)
     HIP_TRY(hipMemcpyAsync(d_tab, disp_table, tab_n * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(d_cond, cond_of_rep, R * 4, hipMemcpyHostToDevice, s));
+  if (int rc = h2d_pinned(ctx, d_cond, cond_of_rep, R * 4, s)) return rc;
   HIP_TRY(hipMemsetAsync(d_fl, 0, 4, s));
   {
     ProfScope ps(ctx, "lrt", n, 1);
@@ -100,12 +101,16 @@ int lrt_run(h3d_ctx* ctx, const int32_t* d_raw, const double* d_f,
 #undef H3D_LRT
   }
   HIP_TRY(hipGetLastError());
-  int fl = 0;
   int tst[kMaxConds];
-  const int tab_check = table_on_dev ? table_status_copy(ctx, tst) : 0;
+  // (the flag and the table status land in pinned memory)
+  int* land = (int*)pinned_rd(ctx, (1 + kMaxConds) * 4);
+  if (!land) return fail(H3D_ENOMEM, "pinned landing zone");
+  const int tab_check = table_on_dev ? table_status_copy(ctx, land + 1) : 0;
   if (tab_check < 0) return tab_check;
-  HIP_TRY(hipMemcpyAsync(&fl, d_fl, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(land, d_fl, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  const int fl = land[0];
+  std::memcpy(tst, land + 1, sizeof(tst));
   if (tab_check) {
     // a device table the host had to redo: the LRT over it again
     const int ts = table_settle(ctx, tst);

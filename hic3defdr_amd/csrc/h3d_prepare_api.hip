@@ -232,16 +232,18 @@ int h3d_disp_pixels_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_col
   int32_t* d_cnt = (int32_t*)scratch(ctx, "dp_cnt", 4);
   double* d_bias = (double*)scratch(ctx, "dp_bias", (size_t)n_bins * R * 8);
   if (!d_sel || !d_cnt || !d_bias) return fail(H3D_ENOMEM, "disp pixel scratch");
-  HIP_TRY(hipMemcpyAsync(d_bias, bias, (size_t)n_bins * R * 8, hipMemcpyHostToDevice, s));
+  if (int rc = h2d_pinned(ctx, d_bias, bias, (size_t)n_bins * R * 8, s)) return rc;
   hipcub::CountingInputIterator<int32_t> it(0);
   size_t tb = 0;
   HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, d_disp_idx, d_sel, d_cnt, (int)n, s));
   void* tmp = scratch(ctx, "cub_tmp_sel", tb);
   if (!tmp) return fail(H3D_ENOMEM, "select temp");
   HIP_TRY(hipcub::DeviceSelect::Flagged(tmp, tb, it, d_disp_idx, d_sel, d_cnt, (int)n, s));
-  int32_t cnt = 0;
-  HIP_TRY(hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, s));
+  int32_t* land = (int32_t*)pinned_rd(ctx, 4);
+  if (!land) return fail(H3D_ENOMEM, "pinned landing zone");
+  HIP_TRY(hipMemcpyAsync(land, d_cnt, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  const int32_t cnt = land[0];
   if (cnt != n_disp)
     return fail(H3D_EARG, "disp_idx selects %d pixels, caller expects %lld", cnt,
                 (long long)n_disp);

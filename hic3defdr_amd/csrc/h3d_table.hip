@@ -807,8 +807,11 @@ extern "C" int h3d_disp_tables_wait(h3d_ctx* ctx) {
   if (!ctx) return fail(H3D_EARG, "null ctx");
   HIP_TRY(hipSetDevice(ctx->device));
   int st[kMaxConds];
-  if (int rc = h3dint::table_status_copy(ctx, st); rc < 0) return rc;
+  int* land = (int*)h3dint::pinned_rd(ctx, sizeof(st));  // pinned: see h2d_pinned
+  if (!land) return fail(H3D_ENOMEM, "pinned landing zone");
+  if (int rc = h3dint::table_status_copy(ctx, land); rc < 0) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  std::memcpy(st, land, sizeof(st));
   if (getenv("H3D_TABLE_STAMPS")) {  // per condition: us since the start
     using h3dtab::kStamps;
     unsigned long long h[kMaxConds * kStamps];
