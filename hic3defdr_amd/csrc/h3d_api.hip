@@ -100,6 +100,15 @@ void* pinned_rd(h3d_ctx* ctx, size_t bytes) {
   return ctx->land;
 }
 
+int d2h_sync(h3d_ctx* ctx, void* dst, const void* d_src, size_t bytes, hipStream_t s) {
+  void* l = pinned_rd(ctx, bytes);
+  if (!l) return fail(H3D_ENOMEM, "pinned landing zone");
+  HIP_TRY(hipMemcpyAsync(l, d_src, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(dst, l, bytes);
+  return 0;
+}
+
 hipEvent_t ev_get(h3d_ctx* ctx) {
   if (!ctx->event_pool.empty()) {
     hipEvent_t e = ctx->event_pool.back();

@@ -179,6 +179,8 @@ int h2d_pinned(h3d_ctx* ctx, void* d_dst, const void* src, size_t bytes, hipStre
 // one user at a time: the caller synchronises before reading it and before
 // its next call), nullptr on failure
 void* pinned_rd(h3d_ctx* ctx, size_t bytes);
+// device -> host copy through the pinned landing zone, synchronous on s
+int d2h_sync(h3d_ctx* ctx, void* dst, const void* d_src, size_t bytes, hipStream_t s);
 // folds the recorded event pairs into ctx->stats (synchronises the stream)
 void prof_collect(h3d_ctx* ctx);
 // grid of a grid-stride elementwise kernel over n items

@@ -5,6 +5,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "h3d.h"
@@ -60,7 +61,7 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
   if (!d_bias || !d_indptr || !d_row || !d_col || !d_val || !d_flag || !d_pos || !d_cnt)
     return fail(H3D_ENOMEM, "union staging");
   P.bias = d_bias;
-  HIP_TRY(hipMemcpyAsync(d_bias, bias, (size_t)n_bins * R * 8, hipMemcpyHostToDevice, s));
+  if (int rc = h2d_pinned(ctx, d_bias, bias, (size_t)n_bins * R * 8, s)) return rc;
   int64_t tot = 0;  // kept entries so far
   int64_t* d_keys = nullptr;
   int32_t* d_ent = nullptr;
@@ -80,9 +81,8 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
     if (!tmps) return fail(H3D_ENOMEM, "scan temp");
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmps, tbs, d_flag, d_pos, (int)m, s));
     int32_t last[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&last[0], d_pos + m - 1, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&last[1], d_flag + m - 1, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = d2h_sync(ctx, &last[0], d_pos + m - 1, 4, s)) return rc;
+    if (int rc = d2h_sync(ctx, &last[1], d_flag + m - 1, 4, s)) return rc;
     const int64_t kept = (int64_t)last[0] + last[1];
     if (tot + kept >= ((int64_t)1 << 31)) return fail(H3D_EARG, "too many in-band entries");
     // the kept-entry arrays grow (keeping what earlier replicates wrote)
@@ -126,8 +126,7 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
   if (!tmp) return fail(H3D_ENOMEM, "scan temp");
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, P.run_of, (int)tot, s));
   int32_t n_runs = 0;
-  HIP_TRY(hipMemcpyAsync(&n_runs, P.run_of + tot - 1, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (int rc = d2h_sync(ctx, &n_runs, P.run_of + tot - 1, 4, s)) return rc;
   P.n_runs = n_runs;
   P.run_start = (int64_t*)scratch(ctx, "u_run_start", std::max<int64_t>(n_runs, 1) * 8);
   int32_t* keep = (int32_t*)scratch(ctx, "u_keep", std::max<int64_t>(n_runs, 1) * 4);
@@ -149,8 +148,7 @@ int h3d_union_count(h3d_ctx* ctx, int R, int n_bins,
   if (!tmp) return fail(H3D_ENOMEM, "scan temp");
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, keep, P.px_of_run, (int)n_runs, s));
   int32_t n_px = 0;
-  HIP_TRY(hipMemcpyAsync(&n_px, P.px_of_run + n_runs - 1, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (int rc = d2h_sync(ctx, &n_px, P.px_of_run + n_runs - 1, 4, s)) return rc;
   P.n_px = n_px;
   *n_px_out = n_px;
   return 0;
@@ -277,8 +275,7 @@ int h3d_pixel_f_dev(h3d_ctx* ctx, const int32_t* d_row, const int32_t* d_dist,
                      d_bad);
   HIP_TRY(hipGetLastError());
   int bad = 0;
-  HIP_TRY(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (int rc = d2h_sync(ctx, &bad, d_bad, 4, s)) return rc;
   if (bad) return fail(H3D_EINPUT, "pixel keys outside the bias / size-factor tables");
   return 0;
 }
@@ -319,9 +316,8 @@ int h3d_scale_disp_dev(h3d_ctx* ctx, const double* d_balanced, const double* d_s
   HIP_TRY(hipGetLastError());
   if (scaled_out)
     HIP_TRY(hipMemcpyAsync(scaled_out, d_scaled, (size_t)n * R * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(flag_out, d_flag, (size_t)n, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return 0;
+  // (the flags through the pinned landing zone: see h2d_pinned)
+  return d2h_sync(ctx, flag_out, d_flag, (size_t)n, s);
 }
 
 int h3d_table_gather_dev(h3d_ctx* ctx, const double* d_tables, int D, int C,
@@ -425,7 +421,7 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
     HIP_TRY(hipMemcpyAsync(d_perm, d_idx, n * 4, hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipMemsetAsync(d_bin, 0, n * 4, s));
   } else {
-    HIP_TRY(hipMemcpyAsync(d_dist, dist, n * 4, hipMemcpyHostToDevice, s));
+    if (int rc = h2d_pinned(ctx, d_dist, dist, n * 4, s)) return rc;
     // stable sort by distance (the pinned equal_bin tie order)
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_dist, d_dist_s, d_idx,
                                                d_perm, (int)n, 0, 31, s));
@@ -449,8 +445,7 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
       HIP_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tb, d_head, d_bin, (int)n, s));
       hipLaunchKernelGGL(k_minus_one, dim3(grid_for(ctx, n)), dim3(kBlock), 0, s, d_bin, n);
       int32_t last = 0;
-      HIP_TRY(hipMemcpyAsync(&last, d_bin + n - 1, 4, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
+      if (int rc = d2h_sync(ctx, &last, d_bin + n - 1, 4, s)) return rc;
       nb = last + 1;
     }
   }
@@ -461,8 +456,7 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
   hipLaunchKernelGGL(k_bin_bounds, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, d_bin,
                      n, nb, d_bstart);
   std::vector<int64_t> bstart(nb + 1);
-  HIP_TRY(hipMemcpyAsync(bstart.data(), d_bstart, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (int rc = d2h_sync(ctx, bstart.data(), d_bstart, (nb + 1) * 8, s)) return rc;
   // 2. per-bin factors s_per_bin (nb, R)
   std::vector<double> spb((size_t)nb * R);
   if (mor) {
@@ -485,8 +479,8 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
         segb[(size_t)r * nb + b] = (int64_t)r * n + bstart[b];
         sege[(size_t)r * nb + b] = (int64_t)r * n + bstart[b + 1];
       }
-    HIP_TRY(hipMemcpyAsync(d_segb, segb.data(), segb.size() * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_sege, sege.data(), sege.size() * 8, hipMemcpyHostToDevice, s));
+    if (int rc = h2d_pinned(ctx, d_segb, segb.data(), segb.size() * 8, s)) return rc;
+    if (int rc = h2d_pinned(ctx, d_sege, sege.data(), sege.size() * 8, s)) return rc;
     tb = 0;
     HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, d_keys, d_keys_s,
                                                        (int)(n * R), nb * R, d_segb,
@@ -498,8 +492,7 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
                                                        d_sege, 0, 64, s));
     hipLaunchKernelGGL(k_mor_median, dim3((nb * R + 255) / 256), dim3(256), 0, s,
                        d_keys_s, d_bstart, d_valid, nb, n, R, d_spb);
-    HIP_TRY(hipMemcpyAsync(spb.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = d2h_sync(ctx, spb.data(), d_spb, (size_t)nb * R * 8, s)) return rc;
   } else {
     // simple_scaling (scaling.py:50-65): column sums over the bin's rows in
     // their original order (members grouped by bin: a stable sort of the
@@ -528,9 +521,7 @@ int size_factors_impl(h3d_ctx* ctx, const double* balanced, const double* d_bala
     hipLaunchKernelGGL(k_bin_colsum, dim3((nb * R + 255) / 256), dim3(256), 0, s, bal,
                        members, d_bstart, nb, R, d_spb);
     std::vector<double> colsum((size_t)nb * R);
-    HIP_TRY(hipMemcpyAsync(colsum.data(), d_spb, (size_t)nb * R * 8, hipMemcpyDeviceToHost,
-                           s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = d2h_sync(ctx, colsum.data(), d_spb, (size_t)nb * R * 8, s)) return rc;
     for (int b = 0; b < nb; ++b) {
       const double* cs = &colsum[(size_t)b * R];
       double lg[kMaxReps];
