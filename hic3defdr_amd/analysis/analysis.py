@@ -232,7 +232,7 @@ class AnalyzingHiC3DeFDR(object):
                 (dist >= self.dist_thresh_min)
         if self.loop_patterns:
             eprint('  making loop_idx', skip=not verbose)
-            loop_idx = pixel_membership(row[disp_idx], col[disp_idx], cl)
+            loop_idx = pixel_membership(row, col, cl, mask=disp_idx)
             self._save_npy(self._npy('loop_idx', chrom), loop_idx, owned=True)
         eprint('  saving data to disk', skip=not verbose)
         for name, a in (('row', row), ('col', col), ('raw', raw),

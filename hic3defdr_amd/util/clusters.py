@@ -219,7 +219,7 @@ def cluster_from_string(cluster_string):
                       .replace(')', ']').replace('}', ']'))
 
 
-def pixel_membership(row, col, clusters_lists, n_bins=None):
+def pixel_membership(row, col, clusters_lists, n_bins=None, mask=None):
     """Boolean vector: (row[k], col[k]) in the union of all clusters
     (reference ``analysis.py:117-125``, a Python set lookup per pixel),
     vectorised with 64-bit pixel keys. ``clusters_lists``: per condition a
@@ -233,21 +233,33 @@ def pixel_membership(row, col, clusters_lists, n_bins=None):
             arrs.append(np.array(sorted(pixels), dtype=np.int64))
     arrs = [a.reshape(-1, 2) for a in arrs if len(a)]
     if not arrs or len(row) == 0:
-        return np.zeros(len(row), dtype=bool)
+        return np.zeros(len(row) if mask is None else
+                        int(np.count_nonzero(mask)), dtype=bool)
     pix = np.concatenate(arrs)
-    return pixel_in(row, col, pix[:, 0], pix[:, 1])
+    return pixel_in(row, col, pix[:, 0], pix[:, 1], mask=mask)
 
 
-def pixel_in(row, col, prow, pcol):
-    """(row[k], col[k]) in the pixel set {(prow, pcol)} (vectorised)."""
-    row = np.asarray(row, dtype=np.int64)
-    col = np.asarray(col, dtype=np.int64)
-    if len(row) == 0 or len(prow) == 0:
-        return np.zeros(len(row), dtype=bool)
+def pixel_in(row, col, prow, pcol, mask=None):
+    """(row[k], col[k]) in the pixel set {(prow, pcol)} (vectorised), for
+    the k where ``mask`` (when given) is set -- the keys are formed over all
+    of row / col in place and masked once (prepare_data's loop_idx over the
+    disp pixels of a chromosome's union)."""
+    row = np.asarray(row)
+    col = np.asarray(col)
+    if mask is not None and len(row):
+        n_out = int(np.count_nonzero(mask))
+    else:
+        n_out = len(row)
+    if n_out == 0 or len(prow) == 0:
+        return np.zeros(n_out, dtype=bool)
     prow = np.asarray(prow, dtype=np.int64)
     pcol = np.asarray(pcol, dtype=np.int64)
     base = int(max(pcol.max(), col.max())) + 1
-    keys = row * base + col
+    keys = row.astype(np.int64)
+    keys *= base
+    keys += col
+    if mask is not None:
+        keys = keys[mask]
     pk = prow * base + pcol
     if len(keys) > 1 and not np.all(keys[1:] > keys[:-1]):
         return np.isin(keys, pk)
